@@ -1,0 +1,331 @@
+#!/usr/bin/env python3
+"""bench.py -- Bloom contains throughput on MI355X (BASELINE.json metric, config C2).
+
+Step = one RBloomFilter.contains(Collection) pass (M/RedissonBloomFilter.java:153-186)
+over a batch of 100M synthetic 32-byte keys (50% previously added) against ONE
+2^32-bit filter with k = 7, keys resident in HBM when the timed region starts.
+
+  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4]
+
+N > 1 is launched by torch.distributed.run, one rank per GPU; C2 does not shard
+("replicas only"), so every rank runs its own replica with its own keys
+(weak scaling) and `value` = keys of all ranks / max-over-ranks time.
+
+Printed JSON (rank 0, one line) carries `roofline` for the dominant kernel
+(k_bloom_contains) from HIP events on the launch stream, and `cpu_baseline`: the
+oracle's single-thread C restatement timed on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
+    p.add_argument("--keys", type=int, default=100_000_000, help="keys per step per GPU (C2)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(world, v: float) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(world, v: int) -> int:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.int64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def load_traffic(path, kernel):
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline: oracle restatement (single thread) on a bounded sample of the same workload
+# ------------------------------------------------------------------------------------------
+def cpu_baseline_c2(target_s: float):
+    import numpy as np
+
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(0x5EED0002)
+    f = O.OracleBloom(1 << 32, 7)
+    # calibrate on 200k keys
+    cal = rng.integers(0, 256, size=(200_000, 32), dtype=np.uint8)
+    f.add(*O.fixed_arena(cal))
+    t0 = time.perf_counter()
+    f.contains(*O.fixed_arena(cal))
+    per_key = (time.perf_counter() - t0) / cal.shape[0]
+    n = int(min(max(target_s / max(per_key, 1e-9), 200_000), 60_000_000))
+    added = rng.integers(0, 256, size=(n // 2, 32), dtype=np.uint8)
+    f.add(*O.fixed_arena(added))
+    probe = np.concatenate([added, rng.integers(0, 256, size=(n - n // 2, 32), dtype=np.uint8)])
+    b, o = O.fixed_arena(probe)
+    t0 = time.perf_counter()
+    c = f.contains(b, o)
+    dt = time.perf_counter() - t0
+    assert c >= n // 2
+    return {"value": n / dt, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"CPU restatement, not reference (Redisson+redis-server absent): oracle/rbx_oracle.c "
+                      f"contains of {n} 32-byte keys (50% present) on a 2^32-bit k=7 bitmap, 1 thread, "
+                      f"{dt:.1f} s"}
+
+
+# ------------------------------------------------------------------------------------------
+# C2: single 2^32-bit filter, batch contains of 100M 32-byte keys
+# ------------------------------------------------------------------------------------------
+def run_c2(args, world, rank, local):
+    import numpy as np
+    import torch
+
+    from redisson_amd import BloomHandle, RedissonClient, device_keys
+    from redisson_amd import _lib as L
+
+    K = 7
+    SIZE = 1 << 32
+    n = args.keys
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    client = RedissonClient(local)
+    f = client.getBloomFilter("bench-c2")
+    f.tryInitRaw(SIZE, K)
+    h = BloomHandle(client, "bench-c2")
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0002 + 1000 * rank)
+    half = n // 2
+    added = torch.randint(0, 256, (half, 32), dtype=torch.uint8, device="cuda", generator=g)
+    fresh = torch.randint(0, 256, (n - half, 32), dtype=torch.uint8, device="cuda", generator=g)
+    probe = torch.cat([added, fresh])
+    del fresh
+    cnt = torch.zeros(4, dtype=torch.int64, device="cuda")
+
+    # setup: add the first half (timed separately: the "add" half of the metric)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    h.add_dev(device_keys(added.data_ptr(), half, 32), cnt.data_ptr(), stream=sptr)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    add_ms = e0.elapsed_time(e1)
+    n_new = int(cnt[0].item())
+
+    dk = device_keys(probe.data_ptr(), n, 32)
+    for _ in range(args.warmup):
+        h.contains_dev(dk, cnt.data_ptr() + 8, stream=sptr)
+    torch.cuda.synchronize()
+    present_one = int(cnt[1].item()) // max(args.warmup, 1) if args.warmup else None
+
+    # random-gather roofline probe at the same working-set size (the 512 MiB bitmap)
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    bm_table = torch.empty(SIZE // 8, dtype=torch.uint8, device="cuda")
+    bm_table.random_(0, 255, generator=g)
+    L.lib().rbx_bench_gather(client.ctx, bm_table.data_ptr(), SIZE // 8, n, K, sink.data_ptr(), sptr)
+    ge0, ge1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ge0.record(stream)
+    for _ in range(3):
+        L.lib().rbx_bench_gather(client.ctx, bm_table.data_ptr(), SIZE // 8, n, K, sink.data_ptr(), sptr)
+    ge1.record(stream)
+    torch.cuda.synchronize()
+    gather_ms = ge0.elapsed_time(ge1) / 3
+    gathers_per_s = n * K / (gather_ms / 1e3)
+    del bm_table
+
+    # timed region
+    cnt[2].zero_()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        h.contains_dev(dk, cnt.data_ptr() + 16, stream=sptr)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    total_present = int(cnt[2].item())
+    if present_one is not None:
+        assert total_present == present_one * args.steps, "contains count changed between steps"
+    assert total_present >= half * args.steps  # no false negatives
+
+    step_s = max_over_ranks(world, max(kern_ms / 1e3, 0.0))
+    keys_all = sum_over_ranks(world, n * args.steps)
+    value = keys_all / (step_s * args.steps)
+    algo_bytes = n * (32 + K * 8)  # 32 B key + k x 8 B gathered per key
+    achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+    traffic = load_traffic(args.traffic_json, "k_bloom_contains")
+    res = {
+        "metric": "Bloom contains keys/sec (whole node), C2: one 2^32-bit filter, k=7, 32-byte keys",
+        "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "C2 RBloomFilter.contains(Collection) of 100M random 32-byte keys "
+                               "(50% present) vs one 2^32-bit k=7 filter per GPU",
+                   "keys_per_gpu": n, "key_bytes": 32, "size_bits": SIZE, "k": K,
+                   "parallelism": f"replicas x{world} (no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": algo_bytes, "kernel": "k_bloom_contains<32,8>",
+                     "kernel_avg_ms": kern_ms,
+                     "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
+        "extra": {"add_keys_per_s_per_gpu": half / (add_ms / 1e3), "add_new_keys": n_new,
+                  "present_per_step": total_present // args.steps, "wall_s_timed": wall},
+    }
+    h.close()
+    client.shutdown()
+    return res
+
+
+# ------------------------------------------------------------------------------------------
+# C4: 10k HLLs, PFADD of 16-byte elements, PFCOUNT of all, RCCL max merge
+# ------------------------------------------------------------------------------------------
+def run_c4(args, world, rank, local):
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from redisson_amd import RedissonClient, device_keys
+    from redisson_amd import _lib as L
+
+    NH = 10_000
+    per = max(1, args.keys // NH)  # elements per HLL per GPU per step
+    n = NH * per
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    client = RedissonClient(local)
+    hs = []
+    for i in range(NH):
+        hp = C.c_void_p()
+        assert L.lib().rbx_hll_open(client.ctx, f"c4-{i}".encode(), 1, C.byref(hp)) == 0
+        hs.append(hp.value)
+    arr = (C.c_void_p * NH)(*hs)
+    seg = np.arange(NH + 1, dtype=np.uint64) * np.uint64(per)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0004 + rank)
+    el = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
+    dk = device_keys(el.data_ptr(), n, 16)
+    for _ in range(args.warmup):
+        assert L.lib().rbx_hll_add_multi_dev(client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk),
+                                             changed.data_ptr(), sptr) == 0
+    torch.cuda.synchronize()
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        assert L.lib().rbx_hll_add_multi_dev(client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk),
+                                             changed.data_ptr(), sptr) == 0
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    out = np.zeros(NH, np.uint64)
+    t0 = time.perf_counter()
+    assert L.lib().rbx_hll_count_each_handles(client.ctx, arr, NH, out.ctypes.data_as(L.u64p)) == 0
+    count_ms = (time.perf_counter() - t0) * 1e3
+    step_s = max_over_ranks(world, ms / 1e3)
+    value = sum_over_ranks(world, n) / step_s
+    achieved = n * 16 / (ms / 1e3) / 1e9
+    res = {
+        "metric": "HLL PFADD elems/sec (whole node), C4: 10k HLLs, 16-byte elements",
+        "value": value, "unit": "elems/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C4 PFADD {per} x 16-byte elements into each of 10k HLLs per GPU",
+                   "elements_per_gpu": n, "parallelism": f"element-partitioned x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, "k_hll_pfadd"),
+                     "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms},
+        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean())},
+    }
+    for hp in hs:
+        L.lib().rbx_hll_close(hp)
+    client.shutdown()
+    return res
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    log(f"[bench] rank {rank}/{world} workload {args.workload}")
+    if args.workload == "c2":
+        res = run_c2(args, world, rank, local)
+        if rank == 0 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_c2(args.cpu_seconds)
+    elif args.workload == "c4":
+        res = run_c4(args, world, rank, local)
+    else:
+        raise SystemExit("c3 bench: see DESIGN.md (round 2)")
+    if rank == 0:
+        res.setdefault("cpu_baseline", None)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,199 @@
+/*
+ * rbx.h -- C ABI of the MI355X-native batched sketch engine (librbx.so).
+ *
+ * Drop-in boundary for Redisson's probabilistic-structure hot path.  Every entry
+ * point below replaces a reference interface; the citation is given per function.
+ * Abbreviation: M/ = /root/reference/redisson/src/main/java/org/redisson/
+ *
+ * Conventions
+ *  - Every function returns int: RBX_OK (0) or a negative error class that mirrors
+ *    the exception the reference throws.  rbx_last_error() returns the message
+ *    (thread-local; valid until the next call on the same thread).
+ *  - The caller owns every host buffer; the library never retains one past return.
+ *    Object handles (rbx_bloom, rbx_hll) are library-owned and reference-counted.
+ *  - Keys/elements are codec OUTPUT bytes (RedissonObject.encode,
+ *    M/RedissonObject.java:319-321).  The engine is codec-agnostic.
+ *  - A context owns one GPU.  Calls on one context are serialized (a batch is the
+ *    unit of serialization, matching the reference's pipeline order); calls from
+ *    several threads are safe.
+ *  - *_dev variants take DEVICE pointers and a hipStream_t (as void*; NULL = the
+ *    context's stream), enqueue work and return without synchronizing.  Counts are
+ *    accumulated into device-resident unsigned long long words.
+ */
+#ifndef RBX_H
+#define RBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBX_ABI_VERSION 1
+
+enum {
+    RBX_OK = 0,
+    RBX_E_ILLEGAL_ARGUMENT = -1, /* java.lang.IllegalArgumentException             */
+    RBX_E_ILLEGAL_STATE = -2,    /* IllegalStateException "Bloom filter is not initialized!" */
+    RBX_E_CONFIG_CHANGED = -3,   /* RedisException "Bloom filter config has been changed" */
+    RBX_E_ARITHMETIC = -4,       /* ArithmeticException "/ by zero" (empty collection) */
+    RBX_E_WRONGTYPE = -5,        /* RedisException WRONGTYPE / INVALIDOBJ            */
+    RBX_E_DEVICE = -6,           /* HIP / RCCL runtime failure                       */
+    RBX_E_OOM = -7,              /* device or host allocation failure                */
+    RBX_E_NO_SUCH_KEY = -8       /* RedisException "ERR no such key" (RENAME)        */
+};
+
+typedef struct rbx_ctx rbx_ctx;
+typedef struct rbx_bloom rbx_bloom;
+typedef struct rbx_hll rbx_hll;
+
+/* A batch of n encoded keys.  Key i is bytes[offsets[i] .. offsets[i+1]) when
+ * offsets != NULL (n+1 entries), else bytes[i*stride .. (i+1)*stride). */
+typedef struct rbx_keys {
+    const uint8_t *bytes;
+    const uint64_t *offsets;
+    uint64_t stride;
+    uint64_t n;
+} rbx_keys;
+
+/* The {name}:config hash (M/RedissonBloomFilter.java:285-288). */
+typedef struct rbx_bloom_config {
+    uint64_t size;               /* "size" (bits)                           */
+    uint32_t hash_iterations;    /* "hashIterations" (k)                    */
+    int64_t expected_insertions; /* "expectedInsertions" (0 if raw-created) */
+    double false_probability;    /* "falseProbability"                      */
+    char false_probability_str[64]; /* BigDecimal.toPlainString form        */
+} rbx_bloom_config;
+
+/* ---- library / context ------------------------------------------------------- */
+int rbx_abi_version(void);
+const char *rbx_last_error(void);
+int rbx_device_count(int *out);
+/* Redisson.create(config) -- M/Redisson.java; one context per GPU. */
+int rbx_init(int device, rbx_ctx **out);
+/* RedissonClient.shutdown() */
+int rbx_shutdown(rbx_ctx *ctx);
+int rbx_synchronize(rbx_ctx *ctx);
+/* The context's hipStream_t, as void*. */
+void *rbx_stream(rbx_ctx *ctx);
+
+/* ---- sharding: M/connection/CRC16.java:51-57, M/cluster/ClusterConnectionManager.java:777-792 */
+uint16_t rbx_crc16(const uint8_t *bytes, size_t len);
+int rbx_calc_slot(const uint8_t *key, size_t len);
+/* Slot range -> GPU of one node: slot * n_gpus / 16384. */
+int rbx_slot_to_gpu(int slot, int n_gpus);
+
+/* ---- Bloom sizing: RedissonBloomFilter.optimalNumOfBits/HashFunctions :79-88 ---- */
+int rbx_bloom_optimal_config(int64_t expected_insertions, double false_probability,
+                             uint64_t *size_out, uint32_t *k_out);
+
+/* ---- RBloomFilter (by name) -- M/api/RBloomFilter.java:27-113 ---------------------- */
+/* tryInit(expectedInsertions, falseProbability)  M/RedissonBloomFilter.java:262-300 */
+int rbx_bloom_try_init(rbx_ctx *ctx, const char *name, int64_t expected_insertions,
+                       double false_probability, int *created);
+/* Engine-level init with a raw (size, k) -- reaches m = 2^32, which tryInit caps at
+ * getMaxSize() = 4,294,967,294 (:257-259). */
+int rbx_bloom_init_raw(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k, int *created);
+/* readConfig() HGETALL {name}:config  :240-255 (RBX_E_ILLEGAL_STATE if absent) */
+int rbx_bloom_read_config(rbx_ctx *ctx, const char *name, rbx_bloom_config *out);
+/* add(Collection) :104-137.  size/k are the caller's cached config, checked like
+ * addConfigCheck :207-213.  out_new (nullable): 1 byte per key, 1 iff the key
+ * counts as newly added under the reference's in-order SETBIT semantics. */
+int rbx_bloom_add(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k,
+                  const rbx_keys *keys, uint8_t *out_new, uint64_t *out_count);
+/* contains(Collection) :153-186.  out_present (nullable): 1 byte per key. */
+int rbx_bloom_contains(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k,
+                       const rbx_keys *keys, uint8_t *out_present, uint64_t *out_count);
+/* count() :215-227 (BITCOUNT + the host double formula) */
+int rbx_bloom_count(rbx_ctx *ctx, const char *name, int64_t *out);
+/* BITCOUNT name */
+int rbx_bloom_bitcount(rbx_ctx *ctx, const char *name, uint64_t *out);
+/* delete() :230-232 -- DEL name {name}:config; *deleted = number of keys removed */
+int rbx_bloom_delete(rbx_ctx *ctx, const char *name, int *deleted);
+/* isExists() :344-347 -- EXISTS name {name}:config > 0 */
+int rbx_bloom_is_exists(rbx_ctx *ctx, const char *name, int *exists);
+/* rename :349-364 and renamenx :366-385 */
+int rbx_bloom_rename(rbx_ctx *ctx, const char *name, const char *new_name);
+int rbx_bloom_renamenx(rbx_ctx *ctx, const char *name, const char *new_name, int *renamed);
+/* GET name: the Redis bitmap string (MSB-first, length = highest SETBIT byte + 1).
+ * Writes min(cap, len) bytes; *redis_len = len. */
+int rbx_bloom_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap, uint64_t *redis_len);
+/* SET name <bytes>: replaces the bitmap string (warm start from Redis data). */
+int rbx_bloom_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint64_t len);
+
+/* ---- Bloom handles and the device-resident batch path ------------------------------ */
+int rbx_bloom_open(rbx_ctx *ctx, const char *name, rbx_bloom **out);
+int rbx_bloom_close(rbx_bloom *b);
+int rbx_bloom_handle_config(const rbx_bloom *b, uint64_t *size, uint32_t *k);
+/* contains over device-resident keys; *d_count += present keys (device word). */
+int rbx_bloom_contains_dev(rbx_ctx *ctx, rbx_bloom *b, const rbx_keys *d_keys,
+                           uint8_t *d_out_present, unsigned long long *d_count, void *stream);
+/* add over device-resident keys; *d_count += newly added keys (device word). */
+int rbx_bloom_add_dev(rbx_ctx *ctx, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out_new,
+                      unsigned long long *d_count, void *stream);
+/* Multi-tenant batch: segment s = keys [seg_offsets[s], seg_offsets[s+1]) tested
+ * against filters[s] -- one Redisson contains(Collection) per segment.
+ * Device pointers: d_seg_offsets (nseg+1 u64), d_counts (nseg u64, accumulated). */
+int rbx_bloom_contains_multi_dev(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
+                                 const uint64_t *d_seg_offsets, const rbx_keys *d_keys,
+                                 uint8_t *d_out_present, unsigned long long *d_counts, void *stream);
+/* add() per segment, segments applied in order (same semantics as nseg calls). */
+int rbx_bloom_add_multi_dev(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
+                            const uint64_t *d_seg_offsets, const rbx_keys *d_keys,
+                            uint8_t *d_out_new, unsigned long long *d_counts, void *stream);
+/* Host-buffer multi-tenant forms (synchronous). */
+int rbx_bloom_contains_multi(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
+                             const uint64_t *seg_offsets, const rbx_keys *keys,
+                             uint8_t *out_present, uint64_t *out_counts);
+int rbx_bloom_add_multi(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
+                        const uint64_t *seg_offsets, const rbx_keys *keys, uint8_t *out_new,
+                        uint64_t *out_counts);
+
+/* ---- RHyperLogLog (by name) -- M/api/RHyperLogLog.java:27-68 -------------------- */
+/* add / addAll -> PFADD name e1..en   M/RedissonHyperLogLog.java:71-81.
+ * *changed = 1 iff the key was created or any register changed. */
+int rbx_hll_add(rbx_ctx *ctx, const char *name, const rbx_keys *elements, int *changed);
+/* A batch of PFADD commands: segment s adds elements [seg_offsets[s], seg_offsets[s+1])
+ * to names[s]; out_changed[s] is the reply of command s (commands apply in order). */
+int rbx_hll_add_multi(rbx_ctx *ctx, const char *const *names, uint32_t nseg,
+                      const uint64_t *seg_offsets, const rbx_keys *elements, uint8_t *out_changed);
+/* count / countWith -> PFCOUNT k1..kn (union when n > 1)  :84-94 */
+int rbx_hll_count(rbx_ctx *ctx, const char *const *names, uint32_t n, uint64_t *out);
+/* n independent single-key PFCOUNTs in one batch (one GPU pass). */
+int rbx_hll_count_each(rbx_ctx *ctx, const char *const *names, uint32_t n, uint64_t *out);
+/* mergeWith -> PFMERGE dest src1..srcn (dest's registers included)  :97-102 */
+int rbx_hll_merge(rbx_ctx *ctx, const char *dest, const char *const *srcs, uint32_t nsrc);
+/* GET name: Redis dense HLL string (16-byte "HYLL" header + 12288 bytes) */
+int rbx_hll_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap, uint64_t *len);
+/* SET name <Redis HLL string> (dense or sparse encoding) */
+int rbx_hll_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint64_t len);
+int rbx_hll_delete(rbx_ctx *ctx, const char *name, int *deleted);
+int rbx_hll_exists(rbx_ctx *ctx, const char *name, int *exists);
+
+/* ---- HLL handles and the device-resident path ------------------------------------- */
+/* Opens (creating an empty HLL if absent and create != 0). */
+int rbx_hll_open(rbx_ctx *ctx, const char *name, int create, rbx_hll **out);
+int rbx_hll_close(rbx_hll *h);
+/* Device address of the 16384 u8 registers (raw, one byte per register). */
+int rbx_hll_registers_dev(rbx_hll *h, void **d_regs);
+/* PFADD batch over device-resident elements; d_changed[s] |= 1 when command s
+ * changed a register.  Each handle may appear at most once per call. */
+int rbx_hll_add_multi_dev(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t nseg,
+                          const uint64_t *d_seg_offsets, const uint64_t *h_seg_offsets,
+                          const rbx_keys *d_elements, uint32_t *d_changed, void *stream);
+/* Single-key PFCOUNT of each handle into host out[i] (synchronous). */
+int rbx_hll_count_each_handles(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n, uint64_t *out);
+
+/* ---- multi-GPU (RCCL over xGMI) ------------------------------------------------------ */
+/* 128-byte ncclUniqueId, created on rank 0 and broadcast by the caller. */
+int rbx_rccl_unique_id(uint8_t out[128]);
+int rbx_rccl_init(rbx_ctx *ctx, const uint8_t id[128], int nranks, int rank);
+/* In-place uint8 MAX all-reduce of the registers of hlls[0..n) across ranks
+ * (ncclAllReduce(ncclUint8, ncclMax)); every rank passes the same names in order. */
+int rbx_hll_allreduce_max(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RBX_H */

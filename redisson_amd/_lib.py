@@ -1,0 +1,128 @@
+"""ctypes binding of librbx.so (include/rbx.h).
+
+The product path runs only through this library: there is no CPU fallback.  If the
+shared object is missing, importing any engine object raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librbx.so")
+
+u8p = C.POINTER(C.c_uint8)
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+ullp = C.POINTER(C.c_ulonglong)
+vp = C.c_void_p
+
+
+class RbxKeys(C.Structure):
+    """struct rbx_keys {bytes, offsets, stride, n}"""
+
+    _fields_ = [("bytes", vp), ("offsets", vp), ("stride", C.c_uint64), ("n", C.c_uint64)]
+
+
+class RbxBloomConfig(C.Structure):
+    _fields_ = [
+        ("size", C.c_uint64),
+        ("hash_iterations", C.c_uint32),
+        ("expected_insertions", C.c_int64),
+        ("false_probability", C.c_double),
+        ("false_probability_str", C.c_char * 64),
+    ]
+
+
+RBX_OK = 0
+RBX_E_ILLEGAL_ARGUMENT = -1
+RBX_E_ILLEGAL_STATE = -2
+RBX_E_CONFIG_CHANGED = -3
+RBX_E_ARITHMETIC = -4
+RBX_E_WRONGTYPE = -5
+RBX_E_DEVICE = -6
+RBX_E_OOM = -7
+RBX_E_NO_SUCH_KEY = -8
+
+# name -> (restype, argtypes); every function declared in include/rbx.h
+SIGNATURES = {
+    "rbx_abi_version": (C.c_int, []),
+    "rbx_last_error": (C.c_char_p, []),
+    "rbx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rbx_init": (C.c_int, [C.c_int, C.POINTER(vp)]),
+    "rbx_shutdown": (C.c_int, [vp]),
+    "rbx_synchronize": (C.c_int, [vp]),
+    "rbx_stream": (vp, [vp]),
+    "rbx_crc16": (C.c_uint16, [u8p, C.c_size_t]),
+    "rbx_calc_slot": (C.c_int, [u8p, C.c_size_t]),
+    "rbx_slot_to_gpu": (C.c_int, [C.c_int, C.c_int]),
+    "rbx_bloom_optimal_config": (C.c_int, [C.c_int64, C.c_double, u64p, u32p]),
+    "rbx_bloom_try_init": (C.c_int, [vp, C.c_char_p, C.c_int64, C.c_double, C.POINTER(C.c_int)]),
+    "rbx_bloom_init_raw": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_bloom_read_config": (C.c_int, [vp, C.c_char_p, C.POINTER(RbxBloomConfig)]),
+    "rbx_bloom_add": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_contains": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_count": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
+    "rbx_bloom_bitcount": (C.c_int, [vp, C.c_char_p, u64p]),
+    "rbx_bloom_delete": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_bloom_is_exists": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_bloom_rename": (C.c_int, [vp, C.c_char_p, C.c_char_p]),
+    "rbx_bloom_renamenx": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_bloom_export": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64, u64p]),
+    "rbx_bloom_import": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64]),
+    "rbx_bloom_open": (C.c_int, [vp, C.c_char_p, C.POINTER(vp)]),
+    "rbx_bloom_close": (C.c_int, [vp]),
+    "rbx_bloom_handle_config": (C.c_int, [vp, u64p, u32p]),
+    "rbx_bloom_contains_dev": (C.c_int, [vp, vp, C.POINTER(RbxKeys), vp, vp, vp]),
+    "rbx_bloom_add_dev": (C.c_int, [vp, vp, C.POINTER(RbxKeys), vp, vp, vp]),
+    "rbx_bloom_contains_multi_dev": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, C.POINTER(RbxKeys), vp, vp, vp]),
+    "rbx_bloom_add_multi_dev": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, C.POINTER(RbxKeys), vp, vp, vp]),
+    "rbx_bloom_contains_multi": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_add_multi": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_hll_add": (C.c_int, [vp, C.c_char_p, C.POINTER(RbxKeys), C.POINTER(C.c_int)]),
+    "rbx_hll_add_multi": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
+    "rbx_hll_count": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p]),
+    "rbx_hll_count_each": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p]),
+    "rbx_hll_merge": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32]),
+    "rbx_hll_export": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64, u64p]),
+    "rbx_hll_import": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64]),
+    "rbx_hll_delete": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_hll_exists": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_hll_open": (C.c_int, [vp, C.c_char_p, C.c_int, C.POINTER(vp)]),
+    "rbx_hll_close": (C.c_int, [vp]),
+    "rbx_hll_registers_dev": (C.c_int, [vp, C.POINTER(vp)]),
+    "rbx_hll_add_multi_dev": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, u64p, C.POINTER(RbxKeys), vp, vp]),
+    "rbx_hll_count_each_handles": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u64p]),
+    "rbx_rccl_unique_id": (C.c_int, [u8p]),
+    "rbx_rccl_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
+    "rbx_hll_allreduce_max": (C.c_int, [vp, C.POINTER(vp), C.c_uint32]),
+    "rbx_bench_gather": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, vp]),
+    # include/rbx_selftest.h
+    "rbx_selftest_mod": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+    "rbx_selftest_hash128": (None, [u8p, C.c_uint64, u64p]),
+    "rbx_selftest_plain_string": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Loads librbx.so (built in-tree by __graft_entry__.build()).  Fails loudly."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build the HIP engine first "
+                "(python -c 'import __graft_entry__ as g; g.build()' or make -C redisson_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    m = lib().rbx_last_error()
+    return m.decode("utf-8", "replace") if m else ""

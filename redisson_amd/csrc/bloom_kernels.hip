@@ -1,0 +1,563 @@
+// bloom_kernels.hip -- RBloomFilter hot path on gfx950.
+//
+// Replaces, per key: Hash.hash128 (M/misc/Hash.java:53-74) -> hash(h1,h2,k,size)
+// (M/RedissonBloomFilter.java:139-151) -> k pipelined SETBIT/GETBIT commands through
+// CommandBatchService (:112-118, :161-167) executed by redis-server's bitops.c.
+//
+// contains: one lane per key, k independent 4-byte gathers in flight per lane.
+// add: the reference counts a key as new iff one of its k SETBIT replies was 0, with
+//   the batch executed strictly in submission order (CommandBatchService.java:115-134,
+//   :335, :600-602).  So key i is new iff some bit b of key i was 0 before the batch
+//   and no earlier key j < i of the batch touches b.  Three steps reproduce that
+//   exactly under full parallelism:
+//     probe : gather the k bits; for every bit that is 0, insert (bit, key) into a
+//             first-setter table with a 64-bit atomicMin on the key id;
+//     commit: a key owning (= minimum id of) any of its zero bits is new; owners
+//             atomicOr their bits into the bitmap.
+//   Keys are processed in chunks that each finish before the next probes, so chunking
+//   preserves the in-order semantics.
+// M/ = /root/reference/redisson/src/main/java/org/redisson/
+#include "rbx_kernels.h"
+
+namespace rbx {
+
+// ---------------------------------------------------------------------------------
+// key hashing dispatch
+// ---------------------------------------------------------------------------------
+template <int KLEN>
+__device__ __forceinline__ void hash_key(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
+    if constexpr (KLEN > 0) {
+        hh128_fixed<KLEN>(keys.bytes + i * (uint64_t)KLEN, h1, h2);
+    } else {
+        uint64_t a, len;
+        if (keys.offsets) {
+            a = keys.offsets[i];
+            len = keys.offsets[i + 1] - a;
+        } else {
+            a = i * keys.stride;
+            len = keys.stride;
+        }
+        hh128_bytes(keys.bytes + a, len, h1, h2);
+    }
+}
+
+__device__ __forceinline__ void block_add_u64(uint64_t v, unsigned long long *dst) {
+    // wave reduce, then one atomic per wave-leader through LDS
+    __shared__ unsigned long long s_part[8];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) s_part[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        const int nw = (blockDim.x + 63) >> 6;
+        for (int w = 0; w < nw; ++w) t += s_part[w];
+        if (t) atomicAdd(dst, t);
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_down(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// The Redis string length only grows; a relaxed read first keeps the atomic off the
+// hot path once the length has saturated (a stale read only costs an extra atomic).
+__device__ __forceinline__ void raise_redis_len(unsigned long long *len, unsigned long long v) {
+    if (v > __hip_atomic_load(len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(len, v);
+}
+
+// Adds val into counts[seg] with one atomic per distinct segment of the wave.
+__device__ __forceinline__ void wave_seg_add(bool active, uint32_t seg, uint32_t val,
+                                             unsigned long long *counts) {
+    uint64_t pending = __ballot(active);
+    while (pending) {
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const uint32_t s = __shfl(seg, leader, 64);
+        const bool mine = active && seg == s;
+        const uint64_t grp = __ballot(mine);
+        const uint64_t hits = __ballot(mine && val);
+        if ((threadIdx.x & 63) == (unsigned)leader && hits) atomicAdd(&counts[s], (unsigned long long)__popcll(hits));
+        pending &= ~grp;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// contains
+// ---------------------------------------------------------------------------------
+// Tests the k bits of one key; KMAX >= k unrolled so all k loads issue before use.
+template <int KMAX>
+__device__ __forceinline__ bool probe_all_set(const uint32_t *__restrict__ bm, const ModParams &mp,
+                                              uint32_t k, uint64_t h1, uint64_t h2) {
+    if constexpr (KMAX > 0) {
+        uint32_t word[KMAX], mask[KMAX];
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
+                word[j] = bm[idx >> 5];
+                mask[j] = bit_in_word(idx);
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        bool all = true;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if ((uint32_t)j < k) all &= (word[j] & mask[j]) != 0u;
+        return all;
+    } else {
+        // any k: 8 loads in flight per round
+        bool all = true;
+        uint64_t h = h1;
+        for (uint32_t j0 = 0; j0 < k; j0 += 8) {
+            uint32_t word[8], mask[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t j = j0 + t;
+                if (j < k) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
+                    word[t] = bm[idx >> 5];
+                    mask[t] = bit_in_word(idx);
+                    h += (j & 1) ? h1 : h2;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (j0 + t < k) all &= (word[t] & mask[t]) != 0u;
+        }
+        return all;
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint32_t *__restrict__ bm,
+                                                        ModParams mp, uint32_t k,
+                                                        uint8_t *__restrict__ out,
+                                                        unsigned long long *__restrict__ count) {
+    uint64_t present = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < keys.n; i += stride) {
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        const bool p = probe_all_set<KMAX>(bm, mp, k, h1, h2);
+        if (out) out[i] = p;
+        present += p;
+    }
+    if (count) block_add_u64(present, count);
+}
+
+// Multi-tenant: segment s = keys [seg_off[s], seg_off[s+1]) against filters[s].
+// A block handles 256 consecutive keys; their segments are found by one global
+// binary search (lane 0) plus an LDS search over the <= 257 segment starts.
+__device__ __forceinline__ uint32_t upper_seg(const uint64_t *off, uint32_t nseg, uint64_t key) {
+    // largest s in [0, nseg) with off[s] <= key   (off[0] = 0 <= key)
+    uint32_t lo = 0, hi = nseg;  // invariant off[lo] <= key < off[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= key) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, const FilterDesc *__restrict__ filt,
+                                                              const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                              uint8_t *__restrict__ out,
+                                                              unsigned long long *__restrict__ counts) {
+    __shared__ uint64_t s_off[257];
+    __shared__ uint32_t s_seg0;
+    const uint64_t nkeys = keys.n;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < nkeys; b0 += (uint64_t)gridDim.x * 256) {
+        if (threadIdx.x == 0) s_seg0 = upper_seg(seg_off, nseg, b0);
+        __syncthreads();
+        const uint32_t s0 = s_seg0;
+        for (uint32_t t = threadIdx.x; t < 257; t += blockDim.x) {
+            const uint32_t s = s0 + t;
+            s_off[t] = s <= nseg ? seg_off[s] : ~0ULL;
+        }
+        __syncthreads();
+        const uint64_t i = b0 + threadIdx.x;
+        const bool active = i < nkeys;
+        uint32_t seg = 0;
+        bool p = false;
+        if (active) {
+            uint32_t lo = 0, hi = 257;  // s_off[lo] <= i < s_off[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_off[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            // lo == 256: more than 256 (empty) segments start inside this block
+            seg = lo < 256 ? s0 + lo : upper_seg(seg_off, nseg, i);
+            const FilterDesc f = filt[seg];
+            uint64_t h1, h2;
+            hash_key<KLEN>(keys, i, h1, h2);
+            p = probe_all_set<KMAX>(f.bm, f.mp, f.k, h1, h2);
+            if (out) out[i] = p;
+        }
+        if (counts) wave_seg_add(active, seg, p, counts);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// add: first-setter table
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ht_slot(uint64_t keypart, uint32_t log2cap) {
+    return (keypart * 0x9E3779B97F4A7C15ULL) >> (64 - log2cap);
+}
+
+// Inserts (keypart, id); the entry's idw ends as min over ids of this epoch.
+__device__ __forceinline__ void ht_insert(HTEntry *__restrict__ T, uint32_t log2cap, uint32_t epoch,
+                                          uint64_t keypart, uint32_t id) {
+    const uint64_t mask = (1ULL << log2cap) - 1;
+    const uint64_t mytag = ((uint64_t)epoch << 56) | keypart;
+    const unsigned long long myidw = ((unsigned long long)(254u - epoch) << 32) | id;
+    uint64_t slot = ht_slot(keypart, log2cap);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        unsigned long long cur = __hip_atomic_load((unsigned long long *)&T[slot].tag, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            if (cur == mytag) {
+                atomicMin((unsigned long long *)&T[slot].idw, myidw);
+                return;
+            }
+            if ((uint32_t)(cur >> 56) == epoch) break;  // occupied by another key this epoch
+            const unsigned long long prev = atomicCAS((unsigned long long *)&T[slot].tag, cur, mytag);
+            if (prev == cur) {
+                atomicMin((unsigned long long *)&T[slot].idw, myidw);
+                return;
+            }
+            cur = prev;  // re-examine this slot
+        }
+        slot = (slot + 1) & mask;
+    }
+}
+
+// Returns the min id recorded for keypart (the entry must exist).
+__device__ __forceinline__ uint32_t ht_owner(const HTEntry *__restrict__ T, uint32_t log2cap, uint32_t epoch,
+                                             uint64_t keypart) {
+    const uint64_t mask = (1ULL << log2cap) - 1;
+    const uint64_t mytag = ((uint64_t)epoch << 56) | keypart;
+    uint64_t slot = ht_slot(keypart, log2cap);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const HTEntry e = T[slot];
+        if (e.tag == mytag) return (uint32_t)e.idw;
+        slot = (slot + 1) & mask;
+    }
+    return 0xffffffffu;
+}
+
+// Probe: gathers the k bits, records which are zero (zmask, bit j <-> hash j) and
+// registers each zero bit in the first-setter table.  Tracks the Redis string length
+// (every SETBIT grows it to idx/8+1, whatever the old bit).
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_add_probe(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                         const FilterDesc *__restrict__ filt,
+                                                         const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                         FilterDesc single, HTEntry *__restrict__ T,
+                                                         uint32_t log2cap, uint32_t epoch,
+                                                         uint32_t *__restrict__ zmask) {
+    static_assert(KMAX > 0 && KMAX <= 32, "probe mask holds 32 hashes");
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        FilterDesc f = single;
+        if (filt) f = filt[upper_seg(seg_off, nseg, i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint32_t maxidx = 0;
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        uint32_t zm = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+                zm |= 1u << j;
+                ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], (uint32_t)t);
+            }
+        }
+        zmask[t] = zm;
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_add_commit(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                          const FilterDesc *__restrict__ filt,
+                                                          const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                          FilterDesc single, const HTEntry *__restrict__ T,
+                                                          uint32_t log2cap, uint32_t epoch,
+                                                          const uint32_t *__restrict__ zmask,
+                                                          uint8_t *__restrict__ out_new,
+                                                          unsigned long long *__restrict__ count,
+                                                          unsigned long long *__restrict__ seg_counts) {
+    uint64_t added = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        const uint32_t zm = zmask[t];
+        bool isnew = false;
+        if (zm) {
+            uint32_t seg = 0;
+            FilterDesc f = single;
+            if (filt) {
+                seg = upper_seg(seg_off, nseg, i);
+                f = filt[seg];
+            }
+            uint64_t h1, h2;
+            hash_key<KLEN>(keys, i, h1, h2);
+            uint64_t h = h1;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((zm >> j) & 1u) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                    if (ht_owner(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx) == (uint32_t)t) {
+                        isnew = true;
+                        atomicOr(&f.bm[idx >> 5], bit_in_word(idx));
+                    }
+                }
+                h += (j & 1) ? h1 : h2;
+            }
+            if (isnew && seg_counts) atomicAdd(&seg_counts[seg], 1ULL);
+        }
+        if (out_new) out_new[i] = isnew;
+        added += isnew;
+    }
+    if (count) block_add_u64(added, count);
+}
+
+// Generic-k add (k > 32): per-pair zero flags in a byte array zflag[t*k + j].
+template <int KLEN>
+__global__ __launch_bounds__(256) void k_bloom_add_probe_anyk(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                              const FilterDesc *__restrict__ filt,
+                                                              const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                              FilterDesc single, HTEntry *__restrict__ T,
+                                                              uint32_t log2cap, uint32_t epoch,
+                                                              uint8_t *__restrict__ zflag, uint32_t kstride) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        FilterDesc f = single;
+        if (filt) f = filt[upper_seg(seg_off, nseg, i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint64_t h = h1;
+        uint32_t maxidx = 0;
+        for (uint32_t j = 0; j < f.k; ++j) {
+            const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+            maxidx = idx > maxidx ? idx : maxidx;
+            const bool z = (f.bm[idx >> 5] & bit_in_word(idx)) == 0u;
+            zflag[t * kstride + j] = z;
+            if (z) ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx, (uint32_t)t);
+            h += (j & 1) ? h1 : h2;
+        }
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+template <int KLEN>
+__global__ __launch_bounds__(256) void k_bloom_add_commit_anyk(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                               const FilterDesc *__restrict__ filt,
+                                                               const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                               FilterDesc single, const HTEntry *__restrict__ T,
+                                                               uint32_t log2cap, uint32_t epoch,
+                                                               const uint8_t *__restrict__ zflag, uint32_t kstride,
+                                                               uint8_t *__restrict__ out_new,
+                                                               unsigned long long *__restrict__ count,
+                                                               unsigned long long *__restrict__ seg_counts) {
+    uint64_t added = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        uint32_t seg = 0;
+        FilterDesc f = single;
+        if (filt) {
+            seg = upper_seg(seg_off, nseg, i);
+            f = filt[seg];
+        }
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint64_t h = h1;
+        bool isnew = false;
+        for (uint32_t j = 0; j < f.k; ++j) {
+            if (zflag[t * kstride + j]) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                if (ht_owner(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx) == (uint32_t)t) {
+                    isnew = true;
+                    atomicOr(&f.bm[idx >> 5], bit_in_word(idx));
+                }
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        if (isnew && seg_counts) atomicAdd(&seg_counts[seg], 1ULL);
+        if (out_new) out_new[i] = isnew;
+        added += isnew;
+    }
+    if (count) block_add_u64(added, count);
+}
+
+// ---------------------------------------------------------------------------------
+// BITCOUNT over nbytes of the bitmap string (RedissonBitSet.cardinalityAsync :482-484)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bitcount(const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                                                  unsigned long long *__restrict__ out) {
+    uint64_t c = 0;
+    const uint64_t nvec = nbytes >> 4;
+    const uint4 *v = (const uint4 *)bytes;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < nvec; i += stride) {
+        const uint4 x = ld_nt16(v + i);
+        c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+    for (uint64_t i = (nvec << 4) + tid; i < nbytes; i += stride) c += __popc((uint32_t)bytes[i]);
+    block_add_u64(c, out);
+}
+
+// ---------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------
+static inline unsigned grid_for(uint64_t n, unsigned cap) {
+    uint64_t g = (n + 255) / 256;
+    if (g == 0) g = 1;
+    return (unsigned)(g < cap ? g : cap);
+}
+
+template <int KLEN>
+static void launch_contains_k(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    if (k <= 8) hipLaunchKernelGGL((k_bloom_contains<KLEN, 8>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+    else if (k <= 16) hipLaunchKernelGGL((k_bloom_contains<KLEN, 16>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+    else hipLaunchKernelGGL((k_bloom_contains<KLEN, 0>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+}
+
+void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st) {
+    const unsigned grid = grid_for(keys.n, kMaxGrid);
+    switch (klen_fast) {
+    case 16: launch_contains_k<16>(keys, bm, mp, k, out, count, st, grid); break;
+    case 32: launch_contains_k<32>(keys, bm, mp, k, out, count, st, grid); break;
+    case 64: launch_contains_k<64>(keys, bm, mp, k, out, count, st, grid); break;
+    default: launch_contains_k<0>(keys, bm, mp, k, out, count, st, grid); break;
+    }
+}
+
+template <int KLEN>
+static void launch_contains_multi_k(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off,
+                                    uint32_t nseg, uint32_t kmax, uint8_t *out, unsigned long long *counts,
+                                    hipStream_t st, unsigned grid) {
+    if (kmax <= 8) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    else if (kmax <= 16) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 0>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+}
+
+void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
+                                 const uint64_t *seg_off, uint32_t nseg, uint32_t kmax, uint8_t *out,
+                                 unsigned long long *counts, hipStream_t st) {
+    const unsigned grid = grid_for(keys.n, kMaxGrid);
+    switch (klen_fast) {
+    case 16: launch_contains_multi_k<16>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
+    case 32: launch_contains_multi_k<32>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
+    case 64: launch_contains_multi_k<64>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
+    default: launch_contains_multi_k<0>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
+    }
+}
+
+template <int KLEN, int KMAX>
+static void launch_add_chunk_k(const AddChunkArgs &a, hipStream_t st) {
+    const unsigned grid = grid_for(a.nchunk, kMaxGrid);
+    hipLaunchKernelGGL((k_bloom_add_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                       a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch, a.zmask);
+    hipLaunchKernelGGL((k_bloom_add_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                       a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch, a.zmask, a.out_new,
+                       a.count, a.seg_counts);
+}
+
+template <int KLEN>
+static void launch_add_chunk_len(const AddChunkArgs &a, hipStream_t st) {
+    if (a.kmax <= 8) launch_add_chunk_k<KLEN, 8>(a, st);
+    else if (a.kmax <= 16) launch_add_chunk_k<KLEN, 16>(a, st);
+    else if (a.kmax <= 32) launch_add_chunk_k<KLEN, 32>(a, st);
+    else {
+        const unsigned grid = grid_for(a.nchunk, kMaxGrid);
+        hipLaunchKernelGGL((k_bloom_add_probe_anyk<KLEN>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                           a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch,
+                           (uint8_t *)a.zmask, a.kmax);
+        hipLaunchKernelGGL((k_bloom_add_commit_anyk<KLEN>), dim3(grid), dim3(256), 0, st, a.keys, a.base,
+                           a.nchunk, a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch,
+                           (const uint8_t *)a.zmask, a.kmax, a.out_new, a.count, a.seg_counts);
+    }
+}
+
+void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st) {
+    switch (klen_fast) {
+    case 16: launch_add_chunk_len<16>(a, st); break;
+    case 32: launch_add_chunk_len<32>(a, st); break;
+    case 64: launch_add_chunk_len<64>(a, st); break;
+    default: launch_add_chunk_len<0>(a, st); break;
+    }
+}
+
+void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st) {
+    const unsigned grid = grid_for((nbytes + 15) / 16, kMaxGrid);
+    hipLaunchKernelGGL(k_bitcount, dim3(grid), dim3(256), 0, st, bytes, nbytes, out);
+}
+
+}  // namespace rbx
+
+// ---------------------------------------------------------------------------------
+// Random-gather roofline probe: the contains kernel's memory pattern with the hashing
+// removed.  Each lane issues k independent 4-byte loads at pseudo-random word offsets
+// of a `nwords`-word table (same MLP structure as k_bloom_contains), XOR-reduced to a
+// sink so nothing is dead-code eliminated.
+// ---------------------------------------------------------------------------------
+namespace rbx {
+template <int K>
+__global__ __launch_bounds__(256) void k_gather_probe(const uint32_t *__restrict__ tbl, uint64_t nwords,
+                                                      uint64_t nkeys, uint64_t seed, uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += stride) {
+        uint64_t z = (seed + i) * 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z ^= z >> 27;
+        uint32_t w[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t r = (uint32_t)(z >> (j & 1 ? 32 : 0)) ^ (uint32_t)(j * 0x9E3779B9u);
+            z += 0x632BE59BD9B4E019ULL;
+            w[j] = tbl[(uint64_t)r * nwords >> 32];
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc ^= w[j];
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;  // practically never taken; keeps the loads live
+}
+
+void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
+                         hipStream_t st) {
+    const unsigned grid = grid_for(nkeys, kMaxGrid);
+    switch (k) {
+    case 10: hipLaunchKernelGGL(k_gather_probe<10>, dim3(grid), dim3(256), 0, st, tbl, nwords, nkeys, 0x5EEDull, sink); break;
+    default: hipLaunchKernelGGL(k_gather_probe<7>, dim3(grid), dim3(256), 0, st, tbl, nwords, nkeys, 0x5EEDull, sink); break;
+    }
+}
+}  // namespace rbx

@@ -1,0 +1,195 @@
+// hll_kernels.hip -- RHyperLogLog hot path on gfx950.
+//
+// Replaces redis-server's PFADD / PFCOUNT / PFMERGE arithmetic [redis-7.2
+// src/hyperloglog.c: MurmurHash64A seed 0xadc83b19, hllPatLen, hllDenseSet, hllCount
+// with the Ertl estimator] that Redisson reaches through RedissonHyperLogLog.addAllAsync /
+// countAsync / mergeWithAsync (M/RedissonHyperLogLog.java:71-102).
+//
+// Device layout: one byte per register (16384 B per HLL); the Redis dense 6-bit
+// string is produced only at export.  PFADD: one workgroup per (command, element tile)
+// keeps the 16384 registers as u32 in LDS (64 KiB), folds every element with
+// ds_max_u32, then merges into HBM with a bytewise-max CAS per 4-register word; the
+// command's reply ("any register changed") is the OR over its tiles.
+// M/ = /root/reference/redisson/src/main/java/org/redisson/
+#include "rbx_kernels.h"
+
+namespace rbx {
+
+constexpr int kHllRegs = 16384;
+constexpr int kPfaddThreads = 1024;
+
+__device__ __forceinline__ uint32_t bytemax4(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = (a >> (8 * i)) & 0xffu, y = (b >> (8 * i)) & 0xffu;
+        r |= (x > y ? x : y) << (8 * i);
+    }
+    return r;
+}
+
+template <int ELEN>
+__device__ __forceinline__ uint64_t elem_hash(const KeysDev &e, uint64_t i) {
+    if constexpr (ELEN > 0) {
+        return murmur_fixed<ELEN>(e.bytes + i * (uint64_t)ELEN);
+    } else {
+        uint64_t a, len;
+        if (e.offsets) {
+            a = e.offsets[i];
+            len = e.offsets[i + 1] - a;
+        } else {
+            a = i * e.stride;
+            len = e.stride;
+        }
+        return murmur_bytes(e.bytes + a, len);
+    }
+}
+
+template <int ELEN>
+__global__ __launch_bounds__(kPfaddThreads) void k_hll_pfadd(KeysDev elems, const HllSeg *__restrict__ tiles,
+                                                             uint32_t *__restrict__ changed) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_regs[];  // 16384 u32
+    const HllSeg tile = tiles[blockIdx.x];
+    uint4 *l4 = (uint4 *)lds_regs;
+    for (int i = threadIdx.x; i < kHllRegs / 4; i += blockDim.x) l4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+
+    uint64_t e = tile.begin + threadIdx.x;
+    // 4 elements per lane per round: loads and hashes overlap before the LDS atomics
+    for (; e + 3ull * blockDim.x < tile.end; e += 4ull * blockDim.x) {
+        uint64_t h[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h[u] = elem_hash<ELEN>(elems, e + (uint64_t)u * blockDim.x);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) atomicMax(&lds_regs[h[u] & (kHllRegs - 1)], hll_count_of(h[u]));
+    }
+    for (; e < tile.end; e += blockDim.x) {
+        const uint64_t h = elem_hash<ELEN>(elems, e);
+        atomicMax(&lds_regs[h & (kHllRegs - 1)], hll_count_of(h));
+    }
+    __syncthreads();
+
+    // merge into the HBM registers (4 registers per u32 word)
+    uint32_t *g = (uint32_t *)tile.regs;
+    int any = 0;
+    for (int w = threadIdx.x; w < kHllRegs / 4; w += blockDim.x) {
+        const uint4 r = l4[w];
+        const uint32_t cand = r.x | (r.y << 8) | (r.z << 16) | (r.w << 24);
+        if (!cand) continue;
+        uint32_t old = g[w];
+        for (;;) {
+            const uint32_t nw = bytemax4(old, cand);
+            if (nw == old) break;
+            const uint32_t prev = atomicCAS(&g[w], old, nw);
+            if (prev == old) {
+                any = 1;
+                break;
+            }
+            old = prev;
+        }
+    }
+    any = __syncthreads_or(any);
+    if (threadIdx.x == 0 && any) atomicOr(&changed[tile.seg], 1u);
+}
+
+void launch_hll_pfadd(const KeysDev &elems, int elen_fast, const HllSeg *d_tiles, uint32_t ntiles,
+                      uint32_t *d_changed, hipStream_t st) {
+    if (!ntiles) return;
+    const size_t lds = kHllRegs * sizeof(uint32_t);
+    switch (elen_fast) {
+    case 16: hipLaunchKernelGGL(k_hll_pfadd<16>, dim3(ntiles), dim3(kPfaddThreads), lds, st, elems, d_tiles, d_changed); break;
+    case 32: hipLaunchKernelGGL(k_hll_pfadd<32>, dim3(ntiles), dim3(kPfaddThreads), lds, st, elems, d_tiles, d_changed); break;
+    case 64: hipLaunchKernelGGL(k_hll_pfadd<64>, dim3(ntiles), dim3(kPfaddThreads), lds, st, elems, d_tiles, d_changed); break;
+    case 8: hipLaunchKernelGGL(k_hll_pfadd<8>, dim3(ntiles), dim3(kPfaddThreads), lds, st, elems, d_tiles, d_changed); break;
+    default: hipLaunchKernelGGL(k_hll_pfadd<0>, dim3(ntiles), dim3(kPfaddThreads), lds, st, elems, d_tiles, d_changed); break;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// PFCOUNT: register histogram + estimator (hllCount), one 256-thread block per HLL.
+// ---------------------------------------------------------------------------------
+__device__ double hll_sigma(double x) {
+    if (x == 1.) return __builtin_inf();
+    double zPrime;
+    double y = 1;
+    double z = x;
+    do {
+        x *= x;
+        zPrime = z;
+        z += x * y;
+        y += y;
+    } while (zPrime != z);
+    return z;
+}
+
+__global__ __launch_bounds__(256) void k_hll_count(uint8_t *const *__restrict__ regs, int *__restrict__ histo,
+                                                   unsigned long long *__restrict__ out) {
+    __shared__ int h[4][64];
+    const uint8_t *r = regs[blockIdx.x];
+    const int wid = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint4 *r4 = (const uint4 *)r;
+    for (int i = threadIdx.x; i < kHllRegs / 16; i += blockDim.x) {
+        const uint4 x = r4[i];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) atomicAdd(&h[wid][(w[j] >> (8 * b)) & 63u], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int t = threadIdx.x;
+        const int s = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        h[0][t] = s;
+        histo[(size_t)blockIdx.x * 64 + t] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int *rh = h[0];
+        if (rh[51] != 0) {  // hllTau path: host evaluates it with glibc pow (redis semantics)
+            out[blockIdx.x] = ~0ULL;
+            return;
+        }
+        const double m = kHllRegs;
+        double z = 0.0;  // m * hllTau(1.0) == 0
+        for (int j = 50; j >= 1; --j) {
+            z += rh[j];
+            z *= 0.5;
+        }
+        z += m * hll_sigma(rh[0] / (double)m);
+        const double E = (double)llround(0.721347520444481703680 * m * m / z);
+        out[blockIdx.x] = (unsigned long long)E;
+    }
+}
+
+void launch_hll_count(uint8_t *const *d_regs, uint32_t n, int *d_histo, unsigned long long *d_out,
+                      hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_hll_count, dim3(n), dim3(256), 0, st, d_regs, d_histo, d_out);
+}
+
+// ---------------------------------------------------------------------------------
+// PFMERGE / union: bytewise max over 16384 registers
+// ---------------------------------------------------------------------------------
+typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void k_hll_merge(uint8_t *__restrict__ dst, uint8_t *const *__restrict__ srcs,
+                                                   uint32_t nsrc, int init_zero) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // one 16-byte vector
+    if (i >= kHllRegs / 16) return;
+    u8x16 acc = init_zero ? (u8x16)(0) : ((const u8x16 *)dst)[i];
+    for (uint32_t s = 0; s < nsrc; ++s) acc = __builtin_elementwise_max(acc, ((const u8x16 *)srcs[s])[i]);
+    ((u8x16 *)dst)[i] = acc;
+}
+
+void launch_hll_merge(uint8_t *dst, uint8_t *const *d_srcs, uint32_t nsrc, hipStream_t st) {
+    hipLaunchKernelGGL(k_hll_merge, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, dst, d_srcs, nsrc, 0);
+}
+
+void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_hll_merge, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, out, d_srcs, nsrc, 1);
+}
+
+}  // namespace rbx

@@ -1,0 +1,1593 @@
+// rbx_api.cpp -- librbx.so host side: contexts, the Redis-like keyspace the sketches
+// live in, batching/chunking, and every extern "C" entry point of include/rbx.h.
+//
+// The keyspace mirrors how Redisson lays the structures out in Redis:
+//   name          -> bitmap string (Bloom) | HLL string
+//   {name}:config -> Bloom config hash    (RedissonObject.suffixName, M/RedissonObject.java:77-82)
+// so delete/exists/rename keep the reference's key-level semantics.
+// M/ = /root/reference/redisson/src/main/java/org/redisson/
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rbx.h"
+#include "rbx_kernels.h"
+
+using namespace rbx;
+
+// =====================================================================================
+// errors
+// =====================================================================================
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(e_ == hipErrorOutOfMemory ? RBX_E_OOM : RBX_E_DEVICE,                  \
+                        std::string(#expr ": ") + hipGetErrorString(e_));                      \
+    } while (0)
+
+#define RBX_TRY(expr)             \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ != RBX_OK) return r_; \
+    } while (0)
+
+// =====================================================================================
+// device buffers
+// =====================================================================================
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int reserve(size_t n) {
+        if (n <= cap) return RBX_OK;
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max<size_t>(n, 4096);
+        HIP_TRY(hipMalloc(&p, want));
+        cap = want;
+        return RBX_OK;
+    }
+    template <class T> T *as() const { return (T *)p; }
+};
+
+// =====================================================================================
+// objects
+// =====================================================================================
+struct BloomConfig {
+    uint64_t size = 0;
+    uint32_t k = 0;
+    int64_t expected = 0;
+    double fpp = 0;
+    std::string fpp_str;
+};
+
+struct Bitmap {  // a Redis string used with SETBIT/GETBIT
+    int device = 0;
+    uint32_t *d_words = nullptr;
+    uint64_t cap_bytes = 0;                 // allocated bytes (multiple of 256)
+    unsigned long long *d_len = nullptr;    // device word: Redis string length
+    ~Bitmap() {
+        if (d_words) (void)hipFree(d_words);
+        if (d_len) (void)hipFree(d_len);
+    }
+};
+
+struct HllState {  // a Redis HLL string, registers unpacked (1 byte each) on the device
+    uint8_t *d_regs = nullptr;  // 16384 bytes inside a pool chunk
+    uint64_t card = 0;          // the header's 8 cached-cardinality bytes (LE); bit 63 = invalid
+    struct rbx_ctx *owner = nullptr;
+    ~HllState();
+};
+
+enum class KType { Config, Bitmap, Hll };
+
+struct Entry {
+    KType type;
+    std::shared_ptr<BloomConfig> cfg;
+    std::shared_ptr<Bitmap> bm;
+    std::shared_ptr<HllState> hll;
+};
+
+struct rbx_bloom {
+    rbx_ctx *ctx;
+    std::string name;
+    uint64_t size;
+    uint32_t k;
+    std::shared_ptr<Bitmap> bm;
+};
+
+struct rbx_hll {
+    rbx_ctx *ctx;
+    std::string name;
+    std::shared_ptr<HllState> st;
+};
+
+struct rbx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    std::unordered_map<std::string, Entry> ks;
+
+    // first-setter table for add()
+    DevBuf table;
+    uint32_t log2cap = 0;
+    uint32_t epoch = 255;  // 255 = table needs (re)initialisation
+    DevBuf zmask;
+
+    // staging for host-buffer calls
+    DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc;
+    std::vector<FilterDesc> filt_cache;  // content of filt_table
+    uint64_t filt_generation = 0;
+    uint64_t generation = 1;  // bumped whenever a bitmap is (re)allocated or freed
+
+    // HLL register pool: chunks of kHllPerChunk x 16 KiB
+    std::vector<uint8_t *> hll_chunks;
+    std::vector<uint8_t *> hll_free;
+
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+static constexpr size_t kHllBytes = 16384;
+static constexpr size_t kHllPerChunk = 4096;  // 64 MiB per pool chunk
+
+HllState::~HllState() {
+    if (d_regs && owner) {
+        std::lock_guard<std::recursive_mutex> g(owner->mu);
+        owner->hll_free.push_back(d_regs);
+    }
+}
+
+static int hll_alloc(rbx_ctx *c, uint8_t **out) {
+    if (c->hll_free.empty()) {
+        uint8_t *chunk = nullptr;
+        HIP_TRY(hipMalloc(&chunk, kHllBytes * kHllPerChunk));
+        c->hll_chunks.push_back(chunk);
+        // hand out in reverse so that successive allocations are ascending
+        for (size_t i = kHllPerChunk; i-- > 0;) c->hll_free.push_back(chunk + i * kHllBytes);
+    }
+    *out = c->hll_free.back();
+    c->hll_free.pop_back();
+    HIP_TRY(hipMemsetAsync(*out, 0, kHllBytes, c->stream));
+    return RBX_OK;
+}
+
+// =====================================================================================
+// helpers
+// =====================================================================================
+static std::string config_name(const std::string &name) {  // suffixName(name, "config")
+    if (name.find('{') != std::string::npos) return name + ":config";
+    return "{" + name + "}:config";
+}
+
+// Java Double.toString digit selection (shortest round-trip, JDK 19+) and
+// BigDecimal.valueOf(d).toPlainString() (M/RedissonBloomFilter.java:288).
+static std::string java_plain_string(double d) {
+    if (d == 0) return std::signbit(d) ? "-0.0" : "0.0";
+    char buf[64];
+    int prec = 1;
+    for (; prec <= 17; ++prec) {
+        snprintf(buf, sizeof buf, "%.*e", prec - 1, d);
+        if (strtod(buf, nullptr) == d) break;
+    }
+    // buf = [-]D.DDDDe[+-]XX
+    std::string s(buf);
+    bool neg = s[0] == '-';
+    if (neg) s = s.substr(1);
+    size_t epos = s.find('e');
+    int exp10 = atoi(s.c_str() + epos + 1);
+    std::string digits;
+    for (size_t i = 0; i < epos; ++i)
+        if (isdigit((unsigned char)s[i])) digits += s[i];
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    // Java: 1e-3 <= |d| < 1e7 -> plain decimal with >= 1 fraction digit; else d.dddE+-n
+    std::string out;
+    double ad = std::fabs(d);
+    if (ad >= 1e-3 && ad < 1e7) {
+        int ip = exp10 + 1;  // digits before the point
+        std::string ipart, fpart;
+        if (ip <= 0) {
+            ipart = "0";
+            fpart = std::string(-ip, '0') + digits;
+        } else if ((size_t)ip >= digits.size()) {
+            ipart = digits + std::string(ip - digits.size(), '0');
+            fpart = "0";
+        } else {
+            ipart = digits.substr(0, ip);
+            fpart = digits.substr(ip);
+        }
+        out = ipart + "." + fpart;
+    } else {
+        // BigDecimal("d.dddE+-n"): unscaled = all digits (>= 2 with the forced ".0"),
+        // scale = fraction digits - n.  toPlainString writes it without exponent.
+        std::string frac = digits.size() > 1 ? digits.substr(1) : "0";
+        std::string unscaled = digits.substr(0, 1) + frac;
+        long scale = (long)frac.size() - exp10;
+        // strip leading zeros of unscaled (never for a nonzero first digit)
+        if (scale <= 0) {
+            out = unscaled + std::string(-scale, '0');
+        } else if ((size_t)scale >= unscaled.size()) {
+            out = "0." + std::string(scale - unscaled.size(), '0') + unscaled;
+        } else {
+            out = unscaled.substr(0, unscaled.size() - scale) + "." + unscaled.substr(unscaled.size() - scale);
+        }
+    }
+    return neg ? "-" + out : out;
+}
+
+// java.lang.Math.round(double), JDK 8+ (round half up, saturating)
+static int64_t java_math_round(double a) {
+    uint64_t bits;
+    memcpy(&bits, &a, 8);
+    int64_t biased = (int64_t)((bits & 0x7ff0000000000000ULL) >> 52);
+    int64_t shift = (52 - 1 + 1023) - biased;
+    if ((shift & -64) == 0) {
+        int64_t r = (int64_t)((bits & 0x000fffffffffffffULL) | 0x0010000000000000ULL);
+        if ((int64_t)bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    if (a != a) return 0;
+    if (a >= 9223372036854775807.0) return INT64_MAX;
+    if (a <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)a;
+}
+
+static int64_t java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+// RedissonBloomFilter.optimalNumOfBits / optimalNumOfHashFunctions (:79-88) and the
+// tryInit validation (:263-277).
+static int optimal_config(int64_t n, double p, uint64_t max_size, uint64_t *size, uint32_t *k) {
+    if (p > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "Bloom filter false probability can't be greater than 1");
+    if (p < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "Bloom filter false probability can't be negative");
+    double pp = p == 0 ? 4.9e-324 : p;
+    volatile double ln2 = std::log(2.0);  // volatile: keep (ln2*ln2) a separate product
+    int64_t s = java_d2l((double)(-n) * std::log(pp) / (ln2 * ln2));
+    if (s == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "Bloom filter calculated size is " + std::to_string(s));
+    if (s < 0 || (uint64_t)s > max_size)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "Bloom filter size can't be greater than " + std::to_string(max_size) +
+                                                ". But calculated size is " + std::to_string(s));
+    int64_t r = java_math_round((double)s / (double)n * ln2);
+    int32_t kk = (int32_t)(uint32_t)(uint64_t)r;
+    if (kk < 1) kk = 1;
+    *size = (uint64_t)s;
+    *k = (uint32_t)kk;
+    return RBX_OK;
+}
+
+static constexpr uint64_t kRedissonMaxSize = 2147483647ULL * 2;  // getMaxSize() :257-259
+static constexpr uint64_t kEngineMaxSize = 1ULL << 32;           // Redis max bit offset + 1
+
+static int set_device(rbx_ctx *c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return RBX_OK;
+}
+
+static hipStream_t pick_stream(rbx_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+static int new_bitmap(rbx_ctx *c, uint64_t size_bits, std::shared_ptr<Bitmap> *out) {
+    auto b = std::make_shared<Bitmap>();
+    b->device = c->device;
+    uint64_t bytes = ((size_bits + 7) / 8 + 255) & ~255ULL;
+    if (bytes == 0) bytes = 256;
+    HIP_TRY(hipMalloc(&b->d_words, bytes));
+    HIP_TRY(hipMalloc(&b->d_len, sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(b->d_words, 0, bytes, c->stream));
+    HIP_TRY(hipMemsetAsync(b->d_len, 0, sizeof(unsigned long long), c->stream));
+    b->cap_bytes = bytes;
+    c->generation++;
+    *out = b;
+    return RBX_OK;
+}
+
+static int grow_bitmap(rbx_ctx *c, Bitmap &b, uint64_t size_bits) {
+    uint64_t bytes = ((size_bits + 7) / 8 + 255) & ~255ULL;
+    if (bytes <= b.cap_bytes) return RBX_OK;
+    uint32_t *nw = nullptr;
+    HIP_TRY(hipMalloc(&nw, bytes));
+    HIP_TRY(hipMemsetAsync(nw, 0, bytes, c->stream));
+    HIP_TRY(hipMemcpyAsync(nw, b.d_words, b.cap_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(b.d_words));
+    b.d_words = nw;
+    b.cap_bytes = bytes;
+    c->generation++;
+    return RBX_OK;
+}
+
+static uint64_t read_dev_u64(rbx_ctx *c, const unsigned long long *p, int *rc) {
+    unsigned long long v = 0;
+    hipError_t e = hipMemcpyAsync(&v, p, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    *rc = e == hipSuccess ? RBX_OK : fail(RBX_E_DEVICE, hipGetErrorString(e));
+    return v;
+}
+
+// exact-match lookups
+static Entry *find(rbx_ctx *c, const std::string &k) {
+    auto it = c->ks.find(k);
+    return it == c->ks.end() ? nullptr : &it->second;
+}
+
+// =====================================================================================
+// key arenas: host -> device staging
+// =====================================================================================
+static int fast_len(const KeysDev &k) {
+    if (k.offsets) return 0;
+    if (((uintptr_t)k.bytes & 15) != 0) return 0;
+    if (k.stride == 16 || k.stride == 32 || k.stride == 64) return (int)k.stride;
+    return 0;
+}
+
+static int fast_len_hll(const KeysDev &k) {
+    if (k.offsets) return 0;
+    if (k.stride == 16 || k.stride == 32 || k.stride == 64) return ((uintptr_t)k.bytes & 15) ? 0 : (int)k.stride;
+    if (k.stride == 8 && ((uintptr_t)k.bytes & 7) == 0) return 8;
+    return 0;
+}
+
+static int validate_keys(const rbx_keys *k) {
+    if (!k) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys is NULL");
+    if (k->n && !k->bytes && !(k->offsets == nullptr && k->stride == 0))
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
+    return RBX_OK;
+}
+
+// Copies keys [i0, i1) of a host arena to device buffers; returns device view with
+// keys renumbered from 0.
+static int upload_keys(rbx_ctx *c, const rbx_keys *k, uint64_t i0, uint64_t i1, KeysDev *out) {
+    uint64_t n = i1 - i0;
+    if (k->offsets) {
+        uint64_t b0 = k->offsets[i0], b1 = k->offsets[i1];
+        RBX_TRY(c->keys_bytes.reserve(b1 - b0 + 16));
+        RBX_TRY(c->keys_offs.reserve((n + 1) * 8));
+        if (b1 > b0) HIP_TRY(hipMemcpyAsync(c->keys_bytes.p, k->bytes + b0, b1 - b0, hipMemcpyHostToDevice, c->stream));
+        std::vector<uint64_t> offs(n + 1);
+        for (uint64_t i = 0; i <= n; ++i) offs[i] = k->offsets[i0 + i] - b0;
+        HIP_TRY(hipMemcpyAsync(c->keys_offs.p, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));  // `offs` is a stack vector
+        *out = KeysDev{c->keys_bytes.as<uint8_t>(), c->keys_offs.as<uint64_t>(), 0, n};
+    } else {
+        uint64_t bytes = n * k->stride;
+        RBX_TRY(c->keys_bytes.reserve(bytes + 16));
+        if (bytes) HIP_TRY(hipMemcpyAsync(c->keys_bytes.p, k->bytes + i0 * k->stride, bytes, hipMemcpyHostToDevice, c->stream));
+        *out = KeysDev{c->keys_bytes.as<uint8_t>(), nullptr, k->stride, n};
+    }
+    return RBX_OK;
+}
+
+static uint64_t chunk_keys_for_upload(const rbx_keys *k, uint64_t i0) {
+    // ~256 MiB of key bytes per upload chunk
+    const uint64_t budget = 256ull << 20;
+    if (!k->offsets) {
+        uint64_t per = k->stride ? budget / k->stride : k->n;
+        return std::max<uint64_t>(1, per);
+    }
+    uint64_t lo = i0, hi = k->n;
+    // largest i1 with offsets[i1] - offsets[i0] <= budget (at least one key)
+    while (hi - lo > 1) {
+        uint64_t mid = (lo + hi) / 2;
+        if (k->offsets[mid] - k->offsets[i0] <= budget) lo = mid;
+        else hi = mid;
+    }
+    uint64_t i1 = (k->offsets[hi] - k->offsets[i0] <= budget) ? hi : lo;
+    return std::max<uint64_t>(1, i1 - i0);
+}
+
+// =====================================================================================
+// add(): chunked probe/commit over the first-setter table
+// =====================================================================================
+static int ensure_table(rbx_ctx *c, uint64_t want_pairs, hipStream_t st) {
+    // capacity >= 2 * pairs per chunk; between 2^16 and 2^27 entries (2 GiB)
+    uint32_t lg = 16;
+    while (lg < 27 && (1ULL << lg) < 2 * want_pairs) ++lg;
+    if (lg > c->log2cap) {
+        RBX_TRY(c->table.reserve(sizeof(HTEntry) << lg));
+        c->log2cap = lg;
+        c->epoch = 255;
+    }
+    if (c->epoch >= 254) {
+        HIP_TRY(hipMemsetAsync(c->table.p, 0xff, sizeof(HTEntry) << c->log2cap, st));
+        c->epoch = 0;
+    } else {
+        c->epoch++;
+    }
+    return RBX_OK;
+}
+
+static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, const uint64_t *d_seg_off,
+                   uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
+                   unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
+    if (keys.n == 0) return RBX_OK;
+    const uint64_t k = std::max<uint32_t>(kmax, 1);
+    // chunk so that pairs per chunk <= 2^26 (table <= 2^27 entries at load <= 1/2)
+    uint64_t chunk = std::min<uint64_t>(keys.n, (1ULL << 26) / k);
+    chunk = std::max<uint64_t>(chunk, 1);
+    const size_t zbytes = kmax <= 32 ? chunk * 4 : chunk * (size_t)kmax;
+    RBX_TRY(c->zmask.reserve(zbytes));
+    const int fl = fast_len(keys);
+    for (uint64_t base = 0; base < keys.n; base += chunk) {
+        const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
+        RBX_TRY(ensure_table(c, nch * k, st));
+        AddChunkArgs a{};
+        a.keys = keys;
+        a.base = base;
+        a.nchunk = nch;
+        a.filt = d_filt;
+        a.seg_off = d_seg_off;
+        a.nseg = nseg;
+        a.single = single;
+        a.table = c->table.as<HTEntry>();
+        a.log2cap = c->log2cap;
+        a.epoch = c->epoch;
+        a.zmask = c->zmask.as<uint32_t>();
+        a.kmax = kmax;
+        a.out_new = d_out_new;
+        a.count = d_count;
+        a.seg_counts = d_seg_counts;
+        launch_bloom_add_chunk(a, fl, st);
+        HIP_TRY(hipGetLastError());
+    }
+    return RBX_OK;
+}
+
+static FilterDesc desc_of(const Bitmap &b, uint64_t size, uint32_t k, uint32_t fid) {
+    FilterDesc f{};
+    f.bm = b.d_words;
+    f.redis_len = b.d_len;
+    f.mp = make_mod_params(size);
+    f.k = k;
+    f.fid = fid;
+    return f;
+}
+
+// =====================================================================================
+// extern "C"
+// =====================================================================================
+extern "C" {
+
+int rbx_abi_version(void) { return RBX_ABI_VERSION; }
+
+const char *rbx_last_error(void) { return g_err.c_str(); }
+
+int rbx_device_count(int *out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (out) *out = n;
+    return RBX_OK;
+}
+
+int rbx_init(int device, rbx_ctx **out) {
+    if (!out) return fail(RBX_E_ILLEGAL_ARGUMENT, "out is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RBX_E_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n) return fail(RBX_E_ILLEGAL_ARGUMENT, "device index out of range");
+    auto *c = new rbx_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(RBX_E_DEVICE, hipGetErrorString(e));
+    }
+    *out = c;
+    return RBX_OK;
+}
+
+int rbx_shutdown(rbx_ctx *c) {
+    if (!c) return RBX_OK;
+    {
+        std::lock_guard<std::recursive_mutex> g(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        if (c->comm) ncclCommDestroy(c->comm);
+        c->ks.clear();
+    }
+    for (auto *p : c->hll_chunks) (void)hipFree(p);
+    c->hll_chunks.clear();
+    c->hll_free.clear();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RBX_OK;
+}
+
+int rbx_synchronize(rbx_ctx *c) {
+    if (!c) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx is NULL");
+    RBX_TRY(set_device(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RBX_OK;
+}
+
+void *rbx_stream(rbx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+// ---- CRC16 / slots --------------------------------------------------------------------
+// XMODEM CRC16 (poly 0x1021, init 0): M/connection/CRC16.java:25-57, table built at load.
+static uint16_t g_crc_table[256];
+static std::once_flag g_crc_once;
+static void build_crc_table() {
+    for (int i = 0; i < 256; ++i) {
+        uint32_t c = (uint32_t)i << 8;
+        for (int b = 0; b < 8; ++b) c = (c & 0x8000) ? ((c << 1) ^ 0x1021) : (c << 1);
+        g_crc_table[i] = (uint16_t)c;
+    }
+}
+
+uint16_t rbx_crc16(const uint8_t *bytes, size_t len) {
+    std::call_once(g_crc_once, build_crc_table);
+    uint32_t crc = 0;
+    for (size_t i = 0; i < len; ++i) crc = ((crc << 8) ^ g_crc_table[((crc >> 8) ^ bytes[i]) & 0xff]) & 0xffff;
+    return (uint16_t)crc;
+}
+
+// calcSlot(byte[]) M/cluster/ClusterConnectionManager.java:777-792 (hashtag rules)
+int rbx_calc_slot(const uint8_t *key, size_t len) {
+    if (!key) return 0;
+    const void *o = memchr(key, '{', len);
+    if (o) {
+        size_t start = (const uint8_t *)o - key;
+        const void *cl = memchr(key, '}', len);  // first '}' anywhere (indexOf from 0)
+        if (cl) {
+            size_t end = (const uint8_t *)cl - key;
+            if (start + 1 < end) return rbx_crc16(key + start + 1, end - start - 1) % 16384;
+        }
+    }
+    return rbx_crc16(key, len) % 16384;
+}
+
+int rbx_slot_to_gpu(int slot, int n_gpus) {
+    if (n_gpus <= 0 || slot < 0 || slot >= 16384) return 0;
+    return (int)((int64_t)slot * n_gpus / 16384);
+}
+
+int rbx_bloom_optimal_config(int64_t n, double p, uint64_t *size, uint32_t *k) {
+    uint64_t s;
+    uint32_t kk;
+    RBX_TRY(optimal_config(n, p, kRedissonMaxSize, &s, &kk));
+    if (size) *size = s;
+    if (k) *k = kk;
+    return RBX_OK;
+}
+
+// ---- Bloom: config ----------------------------------------------------------------------
+static int bloom_init_common(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, int64_t expected,
+                             double fpp, const std::string &fpp_str, int *created) {
+    std::string cn = config_name(name);
+    Entry *e = find(c, cn);
+    if (e) {
+        // Lua: assert(size == false and hashIterations == false) fails -> tryInit returns false
+        if (created) *created = 0;
+        return RBX_OK;
+    }
+    auto cfg = std::make_shared<BloomConfig>();
+    cfg->size = size;
+    cfg->k = k;
+    cfg->expected = expected;
+    cfg->fpp = fpp;
+    cfg->fpp_str = fpp_str;
+    c->ks[cn] = Entry{KType::Config, cfg, nullptr, nullptr};
+    if (created) *created = 1;
+    return RBX_OK;
+}
+
+int rbx_bloom_try_init(rbx_ctx *c, const char *name, int64_t expected, double fpp, int *created) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx/name is NULL");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    uint64_t size;
+    uint32_t k;
+    RBX_TRY(optimal_config(expected, fpp, kRedissonMaxSize, &size, &k));
+    return bloom_init_common(c, name, size, k, expected, fpp, java_plain_string(fpp), created);
+}
+
+int rbx_bloom_init_raw(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, int *created) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx/name is NULL");
+    if (size == 0 || size > kEngineMaxSize) return fail(RBX_E_ILLEGAL_ARGUMENT, "size must be in [1, 2^32]");
+    if (k == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "k must be >= 1");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    return bloom_init_common(c, name, size, k, 0, 0.0, "0.0", created);
+}
+
+static int get_config(rbx_ctx *c, const std::string &name, BloomConfig **out) {
+    Entry *e = find(c, config_name(name));
+    if (!e) return fail(RBX_E_ILLEGAL_STATE, "Bloom filter is not initialized!");
+    if (e->type != KType::Config) return fail(RBX_E_WRONGTYPE, "WRONGTYPE Operation against a key holding the wrong kind of value");
+    *out = e->cfg.get();
+    return RBX_OK;
+}
+
+int rbx_bloom_read_config(rbx_ctx *c, const char *name, rbx_bloom_config *out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    BloomConfig *cfg;
+    RBX_TRY(get_config(c, name, &cfg));
+    out->size = cfg->size;
+    out->hash_iterations = cfg->k;
+    out->expected_insertions = cfg->expected;
+    out->false_probability = cfg->fpp;
+    snprintf(out->false_probability_str, sizeof out->false_probability_str, "%s", cfg->fpp_str.c_str());
+    return RBX_OK;
+}
+
+// addConfigCheck (:207-213): the server-side config must equal the caller's cached copy.
+static int config_check(rbx_ctx *c, const std::string &name, uint64_t size, uint32_t k) {
+    Entry *e = find(c, config_name(name));
+    if (!e || e->type != KType::Config || e->cfg->size != size || e->cfg->k != k)
+        return fail(RBX_E_CONFIG_CHANGED, "Bloom filter config has been changed");
+    return RBX_OK;
+}
+
+// bitmap key for add (created by the first SETBIT) / contains (may be absent)
+static int bitmap_for(rbx_ctx *c, const std::string &name, uint64_t size, bool create,
+                      std::shared_ptr<Bitmap> *out) {
+    Entry *e = find(c, name);
+    if (e) {
+        if (e->type != KType::Bitmap) return fail(RBX_E_WRONGTYPE, "WRONGTYPE Operation against a key holding the wrong kind of value");
+        RBX_TRY(grow_bitmap(c, *e->bm, size));
+        *out = e->bm;
+        return RBX_OK;
+    }
+    if (!create) {
+        out->reset();
+        return RBX_OK;
+    }
+    std::shared_ptr<Bitmap> b;
+    RBX_TRY(new_bitmap(c, size, &b));
+    c->ks[name] = Entry{KType::Bitmap, nullptr, b, nullptr};
+    *out = b;
+    return RBX_OK;
+}
+
+static int bloom_host_op(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                         uint8_t *out_flags, uint64_t *out_count, bool is_add) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx/name is NULL");
+    RBX_TRY(validate_keys(keys));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    // add()/contains() first read the config if the caller has none cached (:106-108)
+    if (size == 0) {
+        BloomConfig *cfg;
+        RBX_TRY(get_config(c, name, &cfg));
+        size = cfg->size;
+        k = cfg->k;
+    }
+    RBX_TRY(config_check(c, name, size, k));
+    if (keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
+    std::shared_ptr<Bitmap> bm;
+    RBX_TRY(bitmap_for(c, name, size, is_add, &bm));
+    if (!bm) {  // GETBIT on a missing key: every bit is 0
+        if (out_flags) memset(out_flags, 0, keys->n);
+        if (out_count) *out_count = 0;
+        return RBX_OK;
+    }
+    RBX_TRY(c->counters.reserve(64));
+    auto *d_count = c->counters.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(d_count, 0, 8, c->stream));
+    FilterDesc f = desc_of(*bm, size, k, 0);
+    for (uint64_t i0 = 0; i0 < keys->n;) {
+        uint64_t n = std::min<uint64_t>(chunk_keys_for_upload(keys, i0), keys->n - i0);
+        KeysDev dk;
+        RBX_TRY(upload_keys(c, keys, i0, i0 + n, &dk));
+        uint8_t *d_out = nullptr;
+        if (out_flags) {
+            RBX_TRY(c->out_bytes.reserve(n));
+            d_out = c->out_bytes.as<uint8_t>();
+        }
+        if (is_add) {
+            RBX_TRY(run_add(c, dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream));
+        } else {
+            launch_bloom_contains(dk, fast_len(dk), f.bm, f.mp, k, d_out, d_count, c->stream);
+            HIP_TRY(hipGetLastError());
+        }
+        if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags + i0, d_out, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        i0 += n;
+    }
+    int rc;
+    uint64_t cnt = read_dev_u64(c, d_count, &rc);
+    RBX_TRY(rc);
+    if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
+    return RBX_OK;
+}
+
+int rbx_bloom_add(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                  uint8_t *out_new, uint64_t *out_count) {
+    return bloom_host_op(c, name, size, k, keys, out_new, out_count, true);
+}
+
+int rbx_bloom_contains(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                       uint8_t *out_present, uint64_t *out_count) {
+    return bloom_host_op(c, name, size, k, keys, out_present, out_count, false);
+}
+
+static int bitcount_locked(rbx_ctx *c, const std::string &name, uint64_t *out) {
+    Entry *e = find(c, name);
+    if (!e) {
+        *out = 0;
+        return RBX_OK;
+    }
+    if (e->type != KType::Bitmap) return fail(RBX_E_WRONGTYPE, "WRONGTYPE Operation against a key holding the wrong kind of value");
+    int rc;
+    uint64_t len = read_dev_u64(c, e->bm->d_len, &rc);
+    RBX_TRY(rc);
+    RBX_TRY(c->counters.reserve(64));
+    auto *d = c->counters.as<unsigned long long>() + 1;
+    HIP_TRY(hipMemsetAsync(d, 0, 8, c->stream));
+    if (len) launch_bitcount((const uint8_t *)e->bm->d_words, len, d, c->stream);
+    HIP_TRY(hipGetLastError());
+    *out = read_dev_u64(c, d, &rc);
+    return rc;
+}
+
+int rbx_bloom_bitcount(rbx_ctx *c, const char *name, uint64_t *out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    return bitcount_locked(c, name, out);
+}
+
+// count() :215-227
+int rbx_bloom_count(rbx_ctx *c, const char *name, int64_t *out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    BloomConfig *cfg;
+    RBX_TRY(get_config(c, name, &cfg));
+    uint64_t bits;
+    RBX_TRY(bitcount_locked(c, name, &bits));
+    double v = (double)(-(int64_t)cfg->size) / ((double)cfg->k) *
+               std::log(1 - (double)bits / ((double)(int64_t)cfg->size));
+    *out = java_math_round(v);
+    return RBX_OK;
+}
+
+static int key_exists(rbx_ctx *c, const std::string &k) { return find(c, k) ? 1 : 0; }
+
+int rbx_bloom_delete(rbx_ctx *c, const char *name, int *deleted) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    int n = 0;
+    n += (int)c->ks.erase(name);
+    n += (int)c->ks.erase(config_name(name));
+    if (n) c->generation++;
+    if (deleted) *deleted = n;
+    return RBX_OK;
+}
+
+int rbx_bloom_is_exists(rbx_ctx *c, const char *name, int *exists) {
+    if (!c || !name || !exists) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    *exists = (key_exists(c, name) + key_exists(c, config_name(name))) > 0;
+    return RBX_OK;
+}
+
+// RENAME semantics: overwrite the target; missing source -> "ERR no such key"
+static int ks_rename(rbx_ctx *c, const std::string &from, const std::string &to) {
+    auto it = c->ks.find(from);
+    if (it == c->ks.end()) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
+    if (from == to) return RBX_OK;
+    Entry e = it->second;
+    c->ks.erase(it);
+    c->ks[to] = e;
+    c->generation++;
+    return RBX_OK;
+}
+
+// renameAsync :349-364 (Lua: rename the bitmap if it exists, then the config)
+int rbx_bloom_rename(rbx_ctx *c, const char *name, const char *new_name) {
+    if (!c || !name || !new_name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (key_exists(c, name)) RBX_TRY(ks_rename(c, name, new_name));
+    return ks_rename(c, config_name(name), config_name(new_name));
+}
+
+// renamenxAsync :366-385 (Lua: renamenx bitmap; if 0 return 0; else renamenx config)
+int rbx_bloom_renamenx(rbx_ctx *c, const char *name, const char *new_name, int *renamed) {
+    if (!c || !name || !new_name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (!key_exists(c, name)) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
+    if (key_exists(c, new_name)) {
+        if (renamed) *renamed = 0;
+        return RBX_OK;
+    }
+    RBX_TRY(ks_rename(c, name, new_name));
+    std::string cf = config_name(name), ct = config_name(new_name);
+    if (!key_exists(c, cf)) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
+    if (key_exists(c, ct)) {
+        if (renamed) *renamed = 0;
+        return RBX_OK;
+    }
+    RBX_TRY(ks_rename(c, cf, ct));
+    if (renamed) *renamed = 1;
+    return RBX_OK;
+}
+
+int rbx_bloom_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *redis_len) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    Entry *e = find(c, name);
+    if (!e) {
+        if (redis_len) *redis_len = 0;
+        return RBX_OK;
+    }
+    if (e->type != KType::Bitmap) return fail(RBX_E_WRONGTYPE, "WRONGTYPE Operation against a key holding the wrong kind of value");
+    int rc;
+    uint64_t len = read_dev_u64(c, e->bm->d_len, &rc);
+    RBX_TRY(rc);
+    if (redis_len) *redis_len = len;
+    uint64_t n = std::min(cap, len);
+    if (out && n) {
+        HIP_TRY(hipMemcpyAsync(out, e->bm->d_words, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return RBX_OK;
+}
+
+int rbx_bloom_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t len) {
+    if (!c || !name || (len && !bytes)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    if (len > (1ULL << 29)) return fail(RBX_E_ILLEGAL_ARGUMENT, "string exceeds the 512 MiB Redis limit");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::shared_ptr<Bitmap> b;
+    uint64_t bits = len * 8;
+    Entry *cfg = find(c, config_name(name));
+    if (cfg && cfg->type == KType::Config) bits = std::max<uint64_t>(bits, cfg->cfg->size);
+    RBX_TRY(new_bitmap(c, bits, &b));
+    if (len) HIP_TRY(hipMemcpyAsync(b->d_words, bytes, len, hipMemcpyHostToDevice, c->stream));
+    unsigned long long L = len;
+    HIP_TRY(hipMemcpyAsync(b->d_len, &L, 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->ks[name] = Entry{KType::Bitmap, nullptr, b, nullptr};
+    return RBX_OK;
+}
+
+// ---- Bloom: handles / device path ---------------------------------------------------------
+int rbx_bloom_open(rbx_ctx *c, const char *name, rbx_bloom **out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    BloomConfig *cfg;
+    RBX_TRY(get_config(c, name, &cfg));
+    std::shared_ptr<Bitmap> bm;
+    RBX_TRY(bitmap_for(c, name, cfg->size, true, &bm));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *out = new rbx_bloom{c, name, cfg->size, cfg->k, bm};
+    return RBX_OK;
+}
+
+int rbx_bloom_close(rbx_bloom *b) {
+    if (!b) return RBX_OK;
+    std::lock_guard<std::recursive_mutex> g(b->ctx->mu);
+    delete b;
+    return RBX_OK;
+}
+
+int rbx_bloom_handle_config(const rbx_bloom *b, uint64_t *size, uint32_t *k) {
+    if (!b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL handle");
+    if (size) *size = b->size;
+    if (k) *k = b->k;
+    return RBX_OK;
+}
+
+static KeysDev keys_dev(const rbx_keys *k) { return KeysDev{k->bytes, k->offsets, k->stride, k->n}; }
+
+int rbx_bloom_contains_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out,
+                           unsigned long long *d_count, void *stream) {
+    if (!c || !b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    RBX_TRY(validate_keys(d_keys));
+    if (d_keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    KeysDev k = keys_dev(d_keys);
+    FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
+    launch_bloom_contains(k, fast_len(k), f.bm, f.mp, b->k, d_out, d_count, pick_stream(c, stream));
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out_new,
+                      unsigned long long *d_count, void *stream) {
+    if (!c || !b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    RBX_TRY(validate_keys(d_keys));
+    if (d_keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    KeysDev k = keys_dev(d_keys);
+    FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
+    return run_add(c, k, nullptr, nullptr, 0, f, b->k, d_out_new, d_count, nullptr, pick_stream(c, stream));
+}
+
+// Uploads the per-segment descriptor table (cached by content + bitmap generation).
+static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, uint32_t *kmax, hipStream_t st) {
+    std::vector<FilterDesc> v(nseg);
+    std::unordered_map<const Bitmap *, uint32_t> fid;
+    uint32_t km = 1;
+    for (uint32_t s = 0; s < nseg; ++s) {
+        rbx_bloom *b = filters[s];
+        if (!b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL filter handle");
+        auto it = fid.find(b->bm.get());
+        uint32_t id = it == fid.end() ? (uint32_t)fid.size() : it->second;
+        if (it == fid.end()) fid[b->bm.get()] = id;
+        if (id >= (1u << 24)) return fail(RBX_E_ILLEGAL_ARGUMENT, "more than 2^24 distinct filters in one call");
+        v[s] = desc_of(*b->bm, b->size, b->k, id);
+        km = std::max(km, b->k);
+    }
+    *kmax = km;
+    bool same = c->filt_generation == c->generation && c->filt_cache.size() == v.size() &&
+                memcmp(c->filt_cache.data(), v.data(), v.size() * sizeof(FilterDesc)) == 0;
+    if (!same) {
+        RBX_TRY(c->filt_table.reserve(v.size() * sizeof(FilterDesc)));
+        HIP_TRY(hipMemcpyAsync(c->filt_table.p, v.data(), v.size() * sizeof(FilterDesc), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        c->filt_cache.swap(v);
+        c->filt_generation = c->generation;
+    }
+    return RBX_OK;
+}
+
+int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg,
+                                 const uint64_t *d_seg_offsets, const rbx_keys *d_keys, uint8_t *d_out,
+                                 unsigned long long *d_counts, void *stream) {
+    if (!c || !filters || !d_seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    RBX_TRY(validate_keys(d_keys));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    hipStream_t st = pick_stream(c, stream);
+    uint32_t kmax;
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
+    if (d_keys->n == 0) return RBX_OK;
+    KeysDev k = keys_dev(d_keys);
+    launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, kmax, d_out,
+                                d_counts, st);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *d_seg_offsets,
+                            const rbx_keys *d_keys, uint8_t *d_out_new, unsigned long long *d_counts,
+                            void *stream) {
+    if (!c || !filters || !d_seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    RBX_TRY(validate_keys(d_keys));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    hipStream_t st = pick_stream(c, stream);
+    uint32_t kmax;
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
+    if (d_keys->n == 0) return RBX_OK;
+    KeysDev k = keys_dev(d_keys);
+    FilterDesc dummy{};
+    return run_add(c, k, c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, dummy, kmax, d_out_new, nullptr,
+                   d_counts, st);
+}
+
+static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *seg_offsets,
+                      const rbx_keys *keys, uint8_t *out_flags, uint64_t *out_counts, bool is_add) {
+    if (!c || !filters || !seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    RBX_TRY(validate_keys(keys));
+    if (seg_offsets[0] != 0 || seg_offsets[nseg] != keys->n)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must span [0, n]");
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (seg_offsets[s + 1] < seg_offsets[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must be ascending");
+        if (seg_offsets[s + 1] == seg_offsets[s]) return fail(RBX_E_ARITHMETIC, "/ by zero");
+    }
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    KeysDev dk;
+    RBX_TRY(upload_keys(c, keys, 0, keys->n, &dk));
+    RBX_TRY(c->seg_offs.reserve((nseg + 1) * 8));
+    HIP_TRY(hipMemcpyAsync(c->seg_offs.p, seg_offsets, (nseg + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    RBX_TRY(c->misc.reserve(nseg * 8));
+    auto *d_counts = c->misc.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(d_counts, 0, nseg * 8, c->stream));
+    uint8_t *d_out = nullptr;
+    if (out_flags) {
+        RBX_TRY(c->out_bytes.reserve(keys->n));
+        d_out = c->out_bytes.as<uint8_t>();
+    }
+    rbx_keys kd{dk.bytes, dk.offsets, dk.stride, dk.n};
+    if (is_add) RBX_TRY(rbx_bloom_add_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts, c->stream));
+    else RBX_TRY(rbx_bloom_contains_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts, c->stream));
+    if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
+    std::vector<unsigned long long> cnt(nseg);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), d_counts, nseg * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out_counts)
+        for (uint32_t s = 0; s < nseg; ++s) out_counts[s] = cnt[s];
+    return RBX_OK;
+}
+
+int rbx_bloom_contains_multi(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *seg_offsets,
+                             const rbx_keys *keys, uint8_t *out_present, uint64_t *out_counts) {
+    return multi_host(c, filters, nseg, seg_offsets, keys, out_present, out_counts, false);
+}
+
+int rbx_bloom_add_multi(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *seg_offsets,
+                        const rbx_keys *keys, uint8_t *out_new, uint64_t *out_counts) {
+    return multi_host(c, filters, nseg, seg_offsets, keys, out_new, out_counts, true);
+}
+
+// ---- HyperLogLog ------------------------------------------------------------------------------
+static constexpr uint64_t kTileElems = 65536;  // elements per PFADD workgroup
+
+static int hll_get(rbx_ctx *c, const std::string &name, bool create, std::shared_ptr<HllState> *out,
+                   bool *created) {
+    if (created) *created = false;
+    Entry *e = find(c, name);
+    if (e) {
+        if (e->type != KType::Hll) return fail(RBX_E_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value.");
+        *out = e->hll;
+        return RBX_OK;
+    }
+    if (!create) {
+        out->reset();
+        return RBX_OK;
+    }
+    auto h = std::make_shared<HllState>();
+    RBX_TRY(hll_alloc(c, &h->d_regs));
+    h->owner = c;
+    h->card = 0;  // createHLLObject: cached cardinality 0, valid
+    c->ks[name] = Entry{KType::Hll, nullptr, nullptr, h};
+    *out = h;
+    if (created) *created = true;
+    return RBX_OK;
+}
+
+// PFADD batch: device elements, commands in order.  Commands naming the same HLL are
+// split into successive launches so each reply sees the previous commands' effect.
+static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64_t *h_seg, const KeysDev &dk,
+                     uint32_t *d_changed, hipStream_t st) {
+    const uint32_t nseg = (uint32_t)hl.size();
+    std::vector<HllSeg> tiles;
+    uint32_t s0 = 0;
+    const int fl = fast_len_hll(dk);
+    while (s0 < nseg) {
+        // a round: maximal run of commands with distinct HLLs
+        std::unordered_map<HllState *, int> seen;
+        uint32_t s1 = s0;
+        while (s1 < nseg && !seen.count(hl[s1])) seen[hl[s1++]] = 1;
+        tiles.clear();
+        for (uint32_t s = s0; s < s1; ++s) {
+            for (uint64_t b = h_seg[s]; b < h_seg[s + 1]; b += kTileElems)
+                tiles.push_back(HllSeg{hl[s]->d_regs, b, std::min(h_seg[s + 1], b + kTileElems), s, 0});
+        }
+        if (!tiles.empty()) {
+            RBX_TRY(c->ptrs.reserve(tiles.size() * sizeof(HllSeg)));
+            HIP_TRY(hipMemcpyAsync(c->ptrs.p, tiles.data(), tiles.size() * sizeof(HllSeg), hipMemcpyHostToDevice, st));
+            launch_hll_pfadd(dk, fl, c->ptrs.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipStreamSynchronize(st));  // tiles vector reused next round
+        }
+        s0 = s1;
+    }
+    return RBX_OK;
+}
+
+int rbx_hll_add_multi(rbx_ctx *c, const char *const *names, uint32_t nseg, const uint64_t *seg_offsets,
+                      const rbx_keys *elements, uint8_t *out_changed) {
+    if (!c || !names || !seg_offsets) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    RBX_TRY(validate_keys(elements));
+    if (nseg == 0) return RBX_OK;
+    if (seg_offsets[0] != 0 || seg_offsets[nseg] != elements->n)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must span [0, n]");
+    for (uint32_t s = 0; s < nseg; ++s)
+        if (seg_offsets[s + 1] < seg_offsets[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must be ascending");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<HllState *> hl(nseg);
+    std::vector<std::shared_ptr<HllState>> keep(nseg);
+    std::vector<uint8_t> created(nseg, 0);
+    for (uint32_t s = 0; s < nseg; ++s) {
+        bool cr;
+        RBX_TRY(hll_get(c, names[s], true, &keep[s], &cr));
+        hl[s] = keep[s].get();
+        created[s] = cr;
+    }
+    RBX_TRY(c->misc.reserve(nseg * 4));
+    auto *d_changed = c->misc.as<uint32_t>();
+    HIP_TRY(hipMemsetAsync(d_changed, 0, nseg * 4, c->stream));
+    auto span_bytes = [&](uint64_t e0, uint64_t e1) {
+        return elements->offsets ? elements->offsets[e1] - elements->offsets[e0] : (e1 - e0) * elements->stride;
+    };
+    const uint64_t budget = 256ull << 20;
+    for (uint32_t s0 = 0; s0 < nseg;) {
+        // commands [s0, s1) whose elements fit one staging upload (at least one command)
+        uint32_t s1 = s0 + 1;
+        while (s1 < nseg && span_bytes(seg_offsets[s0], seg_offsets[s1 + 1]) <= budget) ++s1;
+        const uint64_t e0 = seg_offsets[s0], e1 = seg_offsets[s1];
+        KeysDev dk{};
+        if (e1 > e0) RBX_TRY(upload_keys(c, elements, e0, e1, &dk));
+        std::vector<uint64_t> reb(s1 - s0 + 1);
+        for (uint32_t s = s0; s <= s1; ++s) reb[s - s0] = seg_offsets[s] - e0;
+        std::vector<HllState *> grp(hl.begin() + s0, hl.begin() + s1);
+        RBX_TRY(pfadd_run(c, grp, reb.data(), dk, d_changed + s0, c->stream));
+        s0 = s1;
+    }
+    std::vector<uint32_t> ch(nseg);
+    HIP_TRY(hipMemcpyAsync(ch.data(), d_changed, nseg * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (ch[s]) hl[s]->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+        if (out_changed) out_changed[s] = ch[s] || created[s];
+    }
+    return RBX_OK;
+}
+
+int rbx_hll_add(rbx_ctx *c, const char *name, const rbx_keys *elements, int *changed) {
+    if (!elements) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL elements");
+    uint64_t seg[2] = {0, elements->n};
+    uint8_t ch = 0;
+    RBX_TRY(rbx_hll_add_multi(c, &name, 1, seg, elements, &ch));
+    if (changed) *changed = ch;
+    return RBX_OK;
+}
+
+// glibc-side hllTau fallback and the full estimator from a histogram (redis hllCount)
+static double hll_tau_host(double x) {
+    if (x == 0. || x == 1.) return 0.;
+    double zPrime;
+    double y = 1.0;
+    double z = 1 - x;
+    do {
+        x = std::sqrt(x);
+        zPrime = z;
+        y *= 0.5;
+        z -= std::pow(1 - x, 2) * y;
+    } while (zPrime != z);
+    return z / 3;
+}
+
+static double hll_sigma_host(double x) {
+    if (x == 1.) return INFINITY;
+    double zPrime;
+    double y = 1;
+    double z = x;
+    do {
+        x *= x;
+        zPrime = z;
+        z += x * y;
+        y += y;
+    } while (zPrime != z);
+    return z;
+}
+
+static uint64_t hll_count_from_histo(const int *reghisto) {
+    double m = 16384;
+    double z = m * hll_tau_host((m - reghisto[51]) / (double)m);
+    for (int j = 50; j >= 1; --j) {
+        z += reghisto[j];
+        z *= 0.5;
+    }
+    z += m * hll_sigma_host(reghisto[0] / (double)m);
+    double E = (double)llroundl(0.721347520444481703680 * m * m / z);
+    return (uint64_t)E;
+}
+
+// Computes counts for raw register arrays (device pointers) -> host out.
+static int count_regs(rbx_ctx *c, const std::vector<uint8_t *> &regs, uint64_t *out) {
+    uint32_t n = (uint32_t)regs.size();
+    if (!n) return RBX_OK;
+    RBX_TRY(c->ptrs.reserve(n * sizeof(uint8_t *)));
+    RBX_TRY(c->histo.reserve((size_t)n * 64 * sizeof(int)));
+    RBX_TRY(c->misc.reserve(n * 8));
+    HIP_TRY(hipMemcpyAsync(c->ptrs.p, regs.data(), n * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
+    launch_hll_count(c->ptrs.as<uint8_t *>(), n, c->histo.as<int>(), c->misc.as<unsigned long long>(), c->stream);
+    HIP_TRY(hipGetLastError());
+    std::vector<unsigned long long> res(n);
+    HIP_TRY(hipMemcpyAsync(res.data(), c->misc.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<int> h;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (res[i] == ~0ULL) {  // tau branch: histogram to host, glibc pow
+            if (h.empty()) {
+                h.resize((size_t)n * 64);
+                HIP_TRY(hipMemcpy(h.data(), c->histo.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+            }
+            res[i] = hll_count_from_histo(&h[(size_t)i * 64]);
+        }
+        out[i] = res[i];
+    }
+    return RBX_OK;
+}
+
+// single-key PFCOUNT with the header cache (valid cache -> cached value; else compute+store)
+static int pfcount_each(rbx_ctx *c, const std::vector<HllState *> &hl, uint64_t *out) {
+    std::vector<uint8_t *> regs;
+    std::vector<uint32_t> idx;
+    for (uint32_t i = 0; i < hl.size(); ++i) {
+        if (!hl[i]) {
+            out[i] = 0;
+            continue;
+        }
+        if (!(hl[i]->card >> 63)) {
+            out[i] = hl[i]->card;
+            continue;
+        }
+        regs.push_back(hl[i]->d_regs);
+        idx.push_back(i);
+    }
+    std::vector<uint64_t> r(regs.size());
+    RBX_TRY(count_regs(c, regs, r.data()));
+    for (size_t j = 0; j < idx.size(); ++j) {
+        out[idx[j]] = r[j];
+        hl[idx[j]]->card = r[j];  // store the (valid) cached cardinality
+    }
+    return RBX_OK;
+}
+
+int rbx_hll_count_each(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *out) {
+    if (!c || (n && (!names || !out))) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<HllState *> hl(n);
+    std::vector<std::shared_ptr<HllState>> keep(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        RBX_TRY(hll_get(c, names[i], false, &keep[i], nullptr));
+        hl[i] = keep[i].get();
+    }
+    return pfcount_each(c, hl, out);
+}
+
+int rbx_hll_count(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *out) {
+    if (!c || !names || !out || n == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    if (n == 1) return rbx_hll_count_each(c, names, 1, out);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<std::shared_ptr<HllState>> keep;
+    std::vector<uint8_t *> srcs;
+    for (uint32_t i = 0; i < n; ++i) {
+        std::shared_ptr<HllState> h;
+        RBX_TRY(hll_get(c, names[i], false, &h, nullptr));
+        if (h) {
+            srcs.push_back(h->d_regs);
+            keep.push_back(h);
+        }
+    }
+    if (srcs.empty()) {
+        *out = 0;
+        return RBX_OK;
+    }
+    RBX_TRY(c->ptrs.reserve(srcs.size() * sizeof(uint8_t *)));
+    RBX_TRY(c->out_bytes.reserve(kHllBytes));
+    HIP_TRY(hipMemcpyAsync(c->ptrs.p, srcs.data(), srcs.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
+    launch_hll_union(c->ptrs.as<uint8_t *>(), (uint32_t)srcs.size(), c->out_bytes.as<uint8_t>(), c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<uint8_t *> u{c->out_bytes.as<uint8_t>()};
+    return count_regs(c, u, out);
+}
+
+int rbx_hll_merge(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_t nsrc) {
+    if (!c || !dest || (nsrc && !srcs)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<std::shared_ptr<HllState>> keep;
+    std::vector<uint8_t *> sp;
+    for (uint32_t i = 0; i < nsrc; ++i) {  // type-check every source first (isHLLObjectOrReply)
+        std::shared_ptr<HllState> h;
+        RBX_TRY(hll_get(c, srcs[i], false, &h, nullptr));
+        if (h) {
+            sp.push_back(h->d_regs);
+            keep.push_back(h);
+        }
+    }
+    std::shared_ptr<HllState> d;
+    RBX_TRY(hll_get(c, dest, true, &d, nullptr));
+    if (!sp.empty()) {
+        RBX_TRY(c->ptrs.reserve(sp.size() * sizeof(uint8_t *)));
+        HIP_TRY(hipMemcpyAsync(c->ptrs.p, sp.data(), sp.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
+        launch_hll_merge(d->d_regs, c->ptrs.as<uint8_t *>(), (uint32_t)sp.size(), c->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    d->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+    return RBX_OK;
+}
+
+// Redis dense encoding (HLL_DENSE_SET_REGISTER layout), 16-byte header
+int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *len) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::shared_ptr<HllState> h;
+    RBX_TRY(hll_get(c, name, false, &h, nullptr));
+    if (!h) {
+        if (len) *len = 0;
+        return RBX_OK;
+    }
+    std::vector<uint8_t> regs(kHllBytes);
+    HIP_TRY(hipMemcpyAsync(regs.data(), h->d_regs, kHllBytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> s(16 + 12288 + 1, 0);
+    memcpy(s.data(), "HYLL", 4);
+    s[4] = 0;  // HLL_DENSE
+    for (int i = 0; i < 8; ++i) s[8 + i] = (uint8_t)(h->card >> (8 * i));
+    uint8_t *p = s.data() + 16;
+    for (unsigned long r = 0; r < 16384; ++r) {
+        unsigned long byte = r * 6 / 8, fb = r * 6 & 7, fb8 = 8 - fb, v = regs[r];
+        p[byte] &= (uint8_t)~(63UL << fb);
+        p[byte] |= (uint8_t)(v << fb);
+        p[byte + 1] &= (uint8_t)~(63UL >> fb8);
+        p[byte + 1] |= (uint8_t)(v >> fb8);
+    }
+    if (len) *len = 16 + 12288;
+    if (out) memcpy(out, s.data(), std::min<uint64_t>(cap, 16 + 12288));
+    return RBX_OK;
+}
+
+// accepts the Redis dense and sparse encodings (isHLLObjectOrReply validation)
+int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t len) {
+    if (!c || !name || !bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    const char *bad = "WRONGTYPE Key is not a valid HyperLogLog string value.";
+    if (len < 16 || memcmp(bytes, "HYLL", 4) != 0 || bytes[4] > 1) return fail(RBX_E_WRONGTYPE, bad);
+    std::vector<uint8_t> regs(kHllBytes, 0);
+    if (bytes[4] == 0) {
+        if (len != 16 + 12288) return fail(RBX_E_WRONGTYPE, bad);
+        const uint8_t *p = bytes + 16;
+        for (unsigned long r = 0; r < 16384; ++r) {
+            unsigned long byte = r * 6 / 8, fb = r * 6 & 7, fb8 = 8 - fb;
+            unsigned long b0 = p[byte], b1 = byte + 1 < 12288 ? p[byte + 1] : 0;
+            regs[r] = (uint8_t)(((b0 >> fb) | (b1 << fb8)) & 63);
+        }
+    } else {
+        const uint8_t *p = bytes + 16, *end = bytes + len;
+        uint64_t idx = 0;
+        while (p < end) {
+            uint8_t b = *p;
+            uint64_t run;
+            if ((b & 0xc0) == 0) {  // ZERO
+                run = (b & 0x3f) + 1;
+                p++;
+            } else if ((b & 0xc0) == 0x40) {  // XZERO
+                if (p + 1 >= end) return fail(RBX_E_WRONGTYPE, bad);
+                run = (((uint64_t)(b & 0x3f) << 8) | p[1]) + 1;
+                p += 2;
+            } else {  // VAL
+                run = (b & 3) + 1;
+                uint8_t v = ((b >> 2) & 0x1f) + 1;
+                if (idx + run > 16384) return fail(RBX_E_WRONGTYPE, bad);
+                for (uint64_t j = 0; j < run; ++j) regs[idx + j] = v;
+                p++;
+            }
+            idx += run;
+            if (idx > 16384) return fail(RBX_E_WRONGTYPE, bad);
+        }
+        if (idx != 16384) return fail(RBX_E_WRONGTYPE, bad);
+    }
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    auto it = c->ks.find(name);
+    std::shared_ptr<HllState> h;
+    if (it != c->ks.end() && it->second.type == KType::Hll) {
+        h = it->second.hll;
+    } else {
+        h = std::make_shared<HllState>();
+        RBX_TRY(hll_alloc(c, &h->d_regs));
+        h->owner = c;
+        c->ks[name] = Entry{KType::Hll, nullptr, nullptr, h};
+    }
+    uint64_t card = 0;
+    for (int i = 0; i < 8; ++i) card |= (uint64_t)bytes[8 + i] << (8 * i);
+    h->card = card;
+    HIP_TRY(hipMemcpyAsync(h->d_regs, regs.data(), kHllBytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RBX_OK;
+}
+
+int rbx_hll_delete(rbx_ctx *c, const char *name, int *deleted) {
+    if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    int n = (int)c->ks.erase(name);
+    if (deleted) *deleted = n;
+    return RBX_OK;
+}
+
+int rbx_hll_exists(rbx_ctx *c, const char *name, int *exists) {
+    if (!c || !name || !exists) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    *exists = key_exists(c, name);
+    return RBX_OK;
+}
+
+int rbx_hll_open(rbx_ctx *c, const char *name, int create, rbx_hll **out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::shared_ptr<HllState> h;
+    RBX_TRY(hll_get(c, name, create != 0, &h, nullptr));
+    if (!h) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *out = new rbx_hll{c, name, h};
+    return RBX_OK;
+}
+
+int rbx_hll_close(rbx_hll *h) {
+    if (!h) return RBX_OK;
+    rbx_ctx *c = h->ctx;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    delete h;
+    return RBX_OK;
+}
+
+int rbx_hll_registers_dev(rbx_hll *h, void **d_regs) {
+    if (!h || !d_regs) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    *d_regs = h->st->d_regs;
+    return RBX_OK;
+}
+
+int rbx_hll_add_multi_dev(rbx_ctx *c, rbx_hll *const *hlls, uint32_t nseg, const uint64_t *d_seg_offsets,
+                          const uint64_t *h_seg_offsets, const rbx_keys *d_elements, uint32_t *d_changed,
+                          void *stream) {
+    (void)d_seg_offsets;
+    if (!c || !hlls || !h_seg_offsets || !d_changed) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    RBX_TRY(validate_keys(d_elements));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<HllState *> hl(nseg);
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (!hlls[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL hll handle");
+        hl[s] = hlls[s]->st.get();
+        hl[s]->card |= 1ULL << 63;  // conservatively invalidate (the flags are device-side)
+    }
+    return pfadd_run(c, hl, h_seg_offsets, keys_dev(d_elements), d_changed, pick_stream(c, stream));
+}
+
+int rbx_hll_count_each_handles(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n, uint64_t *out) {
+    if (!c || (n && (!hlls || !out))) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    std::vector<HllState *> hl(n);
+    for (uint32_t i = 0; i < n; ++i) hl[i] = hlls[i] ? hlls[i]->st.get() : nullptr;
+    return pfcount_each(c, hl, out);
+}
+
+// ---- RCCL -----------------------------------------------------------------------------------
+int rbx_rccl_unique_id(uint8_t out[128]) {
+    if (!out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(RBX_E_DEVICE, ncclGetErrorString(r));
+    memcpy(out, id.internal, 128);
+    return RBX_OK;
+}
+
+int rbx_rccl_init(rbx_ctx *c, const uint8_t id[128], int nranks, int rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    ncclUniqueId u;
+    memcpy(u.internal, id, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) return fail(RBX_E_DEVICE, ncclGetErrorString(r));
+    c->nranks = nranks;
+    c->rank = rank;
+    return RBX_OK;
+}
+
+int rbx_hll_allreduce_max(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n) {
+    if (!c || (n && !hlls)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (!c->comm) return fail(RBX_E_ILLEGAL_STATE, "rbx_rccl_init has not been called");
+    RBX_TRY(set_device(c));
+    // coalesce runs of adjacent register blocks into one all-reduce each
+    uint32_t i = 0;
+    ncclGroupStart();
+    while (i < n) {
+        uint8_t *base = hlls[i]->st->d_regs;
+        uint32_t j = i + 1;
+        while (j < n && hlls[j]->st->d_regs == base + (size_t)(j - i) * kHllBytes) ++j;
+        ncclResult_t r = ncclAllReduce(base, base, (size_t)(j - i) * kHllBytes, ncclUint8, ncclMax, c->comm, c->stream);
+        if (r != ncclSuccess) {
+            ncclGroupEnd();
+            return fail(RBX_E_DEVICE, ncclGetErrorString(r));
+        }
+        for (uint32_t t = i; t < j; ++t) hlls[t]->st->card |= 1ULL << 63;
+        i = j;
+    }
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(RBX_E_DEVICE, ncclGetErrorString(r));
+    return RBX_OK;
+}
+
+// ---- self test of the host-compiled device primitives (CPU tests call this) ------------
+// Returns the number of mismatches of mod63 against '%' over `n` pseudo-random pairs.
+uint64_t rbx_selftest_mod(uint64_t n, uint64_t seed) {
+    uint64_t bad = 0, s = seed;
+    auto next = [&]() {
+        uint64_t z = (s += 0x9e3779b97f4a7c15ULL);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+        return z ^ (z >> 31);
+    };
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t d;
+        uint64_t r = next();
+        switch (r & 7) {
+        case 0: d = 1 + (next() & 0xff); break;
+        case 1: d = (1ULL << 32) - (next() & 0xff); break;
+        case 2: d = (1ULL << (1 + (next() % 32))); break;
+        case 3: d = (1ULL << 31) + (next() & 0xffff) - 0x8000; break;
+        default: d = 1 + (next() % (1ULL << 32)); break;
+        }
+        if (d == 0 || d > (1ULL << 32)) d = 1;
+        ModParams p = make_mod_params(d);
+        for (int t = 0; t < 16; ++t) {
+            uint64_t h = next() & 0x7fffffffffffffffULL;
+            if (t == 0) h = 0x7fffffffffffffffULL;
+            if (t == 1) h = d - 1;
+            if (t == 2) h = d;
+            if (mod63(h, p) != (uint32_t)(h % d)) ++bad;
+        }
+    }
+    return bad;
+}
+
+// HighwayHash128 / MurmurHash64A of the host-compiled device code (CPU cross-check).
+void rbx_selftest_hash128(const uint8_t *data, uint64_t len, uint64_t out[2]) {
+    HH s;
+    hh_reset(s);
+    uint64_t i = 0;
+    for (; i + 32 <= len; i += 32) {
+        uint32_t w[8];
+        memcpy(w, data + i, 32);
+        hh_packet(s, w);
+    }
+    uint32_t r = (uint32_t)(len & 31);
+    if (r) {
+        uint32_t t[8] = {0}, p[8];
+        memcpy(t, data + i, r);
+        for (int j = (int)r; j < 32; ++j) ((uint8_t *)t)[j] = 0xA5;  // garbage past the tail
+        hh_tail_packet(t, r, p);
+        hh_remainder_prologue(s, r);
+        hh_packet(s, p);
+    }
+    hh_finalize128(s, out[0], out[1]);
+}
+
+// ---- measurement helpers (include/rbx_bench.h) -----------------------------------------------
+int rbx_bench_gather(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint64_t nkeys, uint32_t k,
+                     void *d_sink, void *stream) {
+    if (!c || !d_table || !d_sink || table_bytes < 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    RBX_TRY(set_device(c));
+    launch_gather_probe((const uint32_t *)d_table, table_bytes / 4, nkeys, k, (uint32_t *)d_sink,
+                        pick_stream(c, stream));
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+// Java BigDecimal.valueOf(d).toPlainString() as stored in the config hash.
+int rbx_selftest_plain_string(double d, char *out, int cap) {
+    std::string s = java_plain_string(d);
+    if (!out || cap <= 0) return (int)s.size();
+    snprintf(out, (size_t)cap, "%s", s.c_str());
+    return (int)s.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// rbx_kernels.h -- shared device structs and kernel launchers (host <-> .hip files).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rbx_device.h"
+
+namespace rbx {
+
+constexpr unsigned kMaxGrid = 2048;  // grid-stride cap: 256 CUs x 8 blocks of 256 threads
+
+struct KeysDev {
+    const uint8_t *bytes;
+    const uint64_t *offsets;  // nullable: fixed stride
+    uint64_t stride;
+    uint64_t n;
+};
+
+// One Bloom filter as the kernels see it (device-resident table for multi-tenant calls).
+struct FilterDesc {
+    uint32_t *bm;                   // bitmap words (Redis string bytes, MSB-first)
+    unsigned long long *redis_len;  // device word: Redis string length in bytes
+    ModParams mp;
+    uint32_t k;
+    uint32_t fid;  // identity in the first-setter table (unique per filter within a call)
+};
+
+struct alignas(16) HTEntry {
+    unsigned long long tag;  // [63:56] epoch, [55:32] fid, [31:0] bit index
+    unsigned long long idw;  // [63:32] 254 - epoch, [31:0] min key id
+};
+
+struct AddChunkArgs {
+    KeysDev keys;
+    uint64_t base, nchunk;
+    const FilterDesc *filt;  // nullable: single filter
+    const uint64_t *seg_off;
+    uint32_t nseg;
+    FilterDesc single;
+    HTEntry *table;
+    uint32_t log2cap, epoch;
+    uint32_t *zmask;  // nchunk words (k <= 32) or nchunk*k bytes
+    uint32_t kmax;
+    uint8_t *out_new;
+    unsigned long long *count;
+    unsigned long long *seg_counts;
+};
+
+// bloom_kernels.hip
+void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
+void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
+                                 const uint64_t *seg_off, uint32_t nseg, uint32_t kmax, uint8_t *out,
+                                 unsigned long long *counts, hipStream_t st);
+void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
+void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
+// random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe
+void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
+                         hipStream_t st);
+
+// hll_kernels.hip
+struct HllSeg {
+    uint8_t *regs;      // 16384 u8 registers
+    uint64_t begin;     // element range [begin, end)
+    uint64_t end;
+    uint32_t seg;       // command index (for the changed flag)
+    uint32_t pad;
+};
+void launch_hll_pfadd(const KeysDev &elems, int elen_fast, const HllSeg *d_tiles, uint32_t ntiles,
+                      uint32_t *d_changed, hipStream_t st);
+// Per-HLL histogram + Redis estimator; out[i] = count, or ~0 when the hllTau branch
+// (a register == 51) must be evaluated on the host with glibc pow.  histo: n*64 ints.
+void launch_hll_count(uint8_t *const *d_regs, uint32_t n, int *d_histo, unsigned long long *d_out,
+                      hipStream_t st);
+// dst = max(dst, src_0..src_{n-1}) over 16384 registers
+void launch_hll_merge(uint8_t *dst, uint8_t *const *d_srcs, uint32_t nsrc, hipStream_t st);
+// raw registers -> scratch union: out = max over a set of HLLs (multi-key PFCOUNT)
+void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipStream_t st);
+
+}  // namespace rbx

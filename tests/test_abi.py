@@ -1,0 +1,83 @@
+"""The C-ABI library loads, exports every symbol include/*.h declares, and its
+host-compiled device primitives agree with the oracle.  CPU only (no compute calls on a GPU)."""
+import ctypes as C
+import glob
+import os
+import re
+
+import numpy as np
+
+from oracle import oracle as O
+from redisson_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        syms |= set(re.findall(r"\b(rbx_[a-z0-9_]+)\s*\(", txt))
+    return syms
+
+
+def test_library_loads_and_exports_all_declared_symbols():
+    lib = L.lib()
+    syms = declared_symbols()
+    assert len(syms) > 40
+    missing = [s for s in sorted(syms) if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the Python binding covers the whole header
+    assert syms <= set(L.SIGNATURES), sorted(syms - set(L.SIGNATURES))
+
+
+def test_abi_version():
+    assert L.lib().rbx_abi_version() == 1
+
+
+def test_fastmod_host_compiled_matches_percent():
+    assert L.lib().rbx_selftest_mod(200_000, 12345) == 0
+
+
+def test_device_hash128_host_compiled_matches_oracle():
+    rng = np.random.default_rng(9)
+    out = (C.c_uint64 * 2)()
+    for ln in list(range(0, 100)) + [127, 128, 129, 1000]:
+        d = rng.bytes(ln)
+        b = (C.c_uint8 * max(1, ln)).from_buffer_copy(d or b"\0")
+        L.lib().rbx_selftest_hash128(b, ln, out)
+        assert (out[0], out[1]) == O.redisson_hash128(d), ln
+
+
+def test_crc16_and_slot_exports():
+    from redisson_amd import calc_slot, crc16, slot_to_gpu
+
+    assert crc16(b"123456789") == 0x31C3
+    for k in [b"foo{bar}baz", b"{}", b"a}b{c}", b"filter", b"{filter}:config", b""]:
+        assert calc_slot(k) == O.calc_slot(k)
+    assert [slot_to_gpu(s, 8) for s in (0, 2047, 2048, 16383)] == [0, 0, 1, 7]
+
+
+def test_false_probability_plain_string():
+    # BigDecimal.valueOf(p).toPlainString() stored in {name}:config (:288)
+    buf = C.create_string_buffer(64)
+    cases = {0.03: "0.03", 0.001: "0.001", 1e-4: "0.00010", 1e-10: "0.00000000010", 0.5: "0.5",
+             1.0: "1.0", 0.0: "0.0", 0.01: "0.01", 1.5e-5: "0.000015", 0.123456789: "0.123456789"}
+    for p, want in cases.items():
+        L.lib().rbx_selftest_plain_string(p, buf, 64)
+        assert buf.value.decode() == want, (p, buf.value)
+
+
+def test_error_mapping_without_gpu():
+    from redisson_amd.exceptions import IllegalArgumentException, raise_for
+
+    s, k = C.c_uint64(), C.c_uint32()
+    rc = L.lib().rbx_bloom_optimal_config(1, 2.0, C.byref(s), C.byref(k))
+    assert rc == L.RBX_E_ILLEGAL_ARGUMENT
+    try:
+        raise_for(rc, L.last_error())
+    except IllegalArgumentException as e:
+        assert "greater than 1" in str(e)
+    rc = L.lib().rbx_bloom_optimal_config(100, 0.03, C.byref(s), C.byref(k))
+    assert rc == 0 and (s.value, k.value) == (729, 5)

@@ -1,0 +1,378 @@
+"""RBloomFilter on the GPU (librbx.so) vs the CPU oracle: bit-exact parity.
+
+Mirrors T/RedissonBloomFilterTest.java (T/ = redisson/src/test/java/org/redisson/) and adds
+per-key parity of contains/add flags, Redis bitmap bytes and count() over many (size, k)
+shapes and key layouts (fast 16/32/64-byte path, unaligned and variable-length generic path).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from redisson_amd import (Arena, ArithmeticException, BloomHandle, IllegalArgumentException,
+                          IllegalStateException, RedisException, bloom_add_multi, bloom_contains_multi)
+
+pytestmark = pytest.mark.gpu
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+# ---- T/RedissonBloomFilterTest.java replays ----------------------------------------------
+def test_contains_all(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    lst = ["1", "2", "3"]
+    assert f.contains(lst) == 0
+    assert f.add(lst) == 3
+    assert f.contains(lst) == 3
+    assert f.contains(["1", "5"]) == 1
+
+
+def test_add_all(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    lst = ["1", "2", "3"]
+    assert f.add(lst) == 3
+    assert f.add(lst) == 0
+    assert f.count() == 3
+    assert f.add(["1", "5"]) == 1
+    assert f.count() == 4
+    for s in lst:
+        assert f.contains(s) is True
+
+
+@pytest.mark.parametrize("n,p", [(1, -1), (1, 2), (1, 1)])
+def test_illegal_arguments(client, fresh, n, p):
+    with pytest.raises(IllegalArgumentException):
+        client.getBloomFilter(fresh).tryInit(n, p)
+
+
+def test_config(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    assert f.getExpectedInsertions() == 100
+    assert f.getFalseProbability() == 0.03
+    assert f.getHashIterations() == 5
+    assert f.getSize() == 729
+
+
+def test_init(client, fresh):
+    f = client.getBloomFilter(fresh)
+    assert f.tryInit(55000000, 0.03) is True
+    assert f.tryInit(55000001, 0.03) is False
+    f.delete()
+    assert f.isExists() is False
+    assert f.tryInit(55000001, 0.03) is True
+    f.delete()
+
+
+@pytest.mark.parametrize("op", ["getExpectedInsertions", "contains", "add"])
+def test_not_initialized(client, fresh, op):
+    f = client.getBloomFilter(fresh)
+    with pytest.raises(IllegalStateException):
+        if op == "getExpectedInsertions":
+            f.getExpectedInsertions()
+        else:
+            getattr(f, op)("32")
+
+
+def test_empty_rename(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(1000, 0.01)
+    f.rename(fresh + "1")
+    assert f.isExists()
+    assert client.getBloomFilter(fresh).isExists() is False
+    f.delete()
+
+
+def _test_body(f):  # RedissonBloomFilterTest.test(RBloomFilter)
+    assert f.contains("123") is False
+    assert f.add("123") is True
+    assert f.contains("123") is True
+    assert f.add("123") is False
+    assert f.count() == 1
+    assert f.contains("hflgs;jl;ao1-32471320o31803-24") is False
+    assert f.add("hflgs;jl;ao1-32471320o31803-24") is True
+    assert f.contains("hflgs;jl;ao1-32471320o31803-24") is True
+    assert f.count() == 2
+
+
+def test_large_filters(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(550000000, 0.5)
+    _test_body(f)
+    f.delete()
+    assert f.tryInit(550000000, 0.03) is True
+    _test_body(f)
+    f.delete()
+
+
+def test_rename(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(550000000, 0.03)
+    assert f.add("123") is True
+    f.rename(fresh + "new")
+    f2 = client.getBloomFilter(fresh + "new")
+    assert f2.count() == 1
+    assert client.getBloomFilter(fresh).isExists() is False
+    f2.delete()
+
+
+def test_renamenx(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(550000000, 0.03)
+    assert f.add("123") is True
+    assert f.contains("123") is True
+    f2 = client.getBloomFilter(fresh + "2")
+    f2.tryInit(550000000, 0.03)
+    assert f2.add("234") is True
+    assert f.renamenx(fresh + "2") is False
+    assert f.count() == 1
+    assert f.renamenx(fresh + "new") is True
+    assert client.getBloomFilter(fresh).isExists() is False
+    nf = client.getBloomFilter(fresh + "new")
+    assert nf.count() == 1
+    assert nf.contains("123") is True
+    nf.delete()
+    f2.delete()
+
+
+# ---- reference error behaviour ------------------------------------------------------------
+def test_empty_collection_arithmetic(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    with pytest.raises(ArithmeticException):
+        f.add([])
+    with pytest.raises(ArithmeticException):
+        f.contains([])
+    f.delete()
+
+
+def test_config_changed(client, fresh):
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    f.add(["a"])
+    other = client.getBloomFilter(fresh)
+    other.delete()
+    other.tryInit(1000, 0.01)
+    with pytest.raises(RedisException, match="config has been changed"):
+        f.add(["b"])
+    with pytest.raises(RedisException, match="config has been changed"):
+        f.contains(["b"])
+    other.delete()
+
+
+def test_wrongtype(client, fresh):
+    h = client.getHyperLogLog(fresh)
+    h.add("x")
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100, 0.03)
+    with pytest.raises(RedisException, match="WRONGTYPE"):
+        f.add(["a"])
+    f.delete()
+
+
+# ---- parity against the oracle -----------------------------------------------------------------
+def _oargs(a):
+    """oracle (bytes, offsets) for a list of keys or an Arena."""
+    if isinstance(a, list):
+        return O.arena(a)
+    if a.offsets is None:
+        stride = a.struct.stride
+        return a.bytes, np.arange(a.n + 1, dtype=np.uint64) * np.uint64(stride)
+    return a.bytes, a.offsets
+
+
+def _parity(client, name, size, k, batches, probes):
+    f = client.getBloomFilter(name)
+    assert f.tryInitRaw(size, k)
+    ref = O.OracleBloom(size, k)
+    for b in batches:
+        cg, ng = f.addEach(Arena(b) if isinstance(b, list) else b)
+        cr, nr = ref.add(*_oargs(b), per_key=True)
+        assert cg == cr
+        assert np.array_equal(ng, nr)
+    for p in probes:
+        cg, pg = f.containsEach(Arena(p) if isinstance(p, list) else p)
+        cr, pr = ref.contains(*_oargs(p), per_key=True)
+        assert cg == cr
+        assert np.array_equal(pg, pr)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.bitcount() == ref.bitcount()
+    f.delete()
+
+
+SHAPES = [(729, 5), (64, 7), (9585, 7), (95850583, 7), (14377587, 10), (1 << 20, 7), (1000003, 1),
+          (100003, 17), (100003, 33), (50021, 40), (4294967293, 7), (1 << 32, 7), (3, 3), (1, 4)]
+
+
+@pytest.mark.parametrize("size,k", SHAPES)
+def test_parity_variable_length(client, fresh, size, k):
+    rng = np.random.default_rng(size * 31 + k)
+    base = [rng.bytes(int(L)) for L in rng.integers(0, 100, size=3000)]
+    batches = [[base[int(j)] for j in rng.integers(0, len(base), size=2000)] for _ in range(3)]
+    probes = [base[:1500] + [rng.bytes(int(L)) for L in rng.integers(0, 100, size=1500)]]
+    _parity(client, fresh, size, k, batches, probes)
+
+
+@pytest.mark.parametrize("L", [16, 32, 64, 24, 48, 8])
+@pytest.mark.parametrize("size,k", [(95850583, 7), (14377587, 10), (1 << 32, 7), (1000, 40)])
+def test_parity_fixed_length(client, fresh, L, size, k):
+    rng = np.random.default_rng(L * 1000 + k)
+    mat = rng.integers(0, 256, size=(20000, L), dtype=np.uint8)
+    mat[5000:5100] = mat[0:100]  # duplicates inside the batch
+    a1 = Arena.fixed(mat[:12000])
+    a2 = Arena.fixed(mat[8000:])
+    probe = Arena.fixed(np.concatenate([mat[:3000], rng.integers(0, 256, size=(3000, L), dtype=np.uint8)]))
+    _parity(client, fresh, size, k, [a1, a2], [probe])
+
+
+def test_parity_unaligned_device_keys(client, fresh):
+    """32-byte keys at an odd device address (generic unaligned path) and variable-length
+    keys through the device offsets arena."""
+    import torch
+
+    from redisson_amd import device_keys
+
+    rng = np.random.default_rng(77)
+    n = 4000
+    raw = rng.integers(0, 256, size=(1 + n * 32), dtype=np.uint8)
+    mat = np.ascontiguousarray(raw[1:].reshape(n, 32))
+    d = torch.from_numpy(raw).cuda()
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(95850583, 7)
+    h = BloomHandle(client, fresh)
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    h.add_dev(device_keys(d.data_ptr() + 1, n, 32), cnt.data_ptr(), out.data_ptr())
+    client.synchronize()
+    ref = O.OracleBloom(95850583, 7)
+    cr, nr = ref.add(*O.fixed_arena(mat), per_key=True)
+    assert cnt[0].item() == cr and np.array_equal(out.cpu().numpy(), nr)
+    # variable-length keys through device offsets
+    keys = [rng.bytes(int(L)) for L in rng.integers(0, 90, size=n)]
+    b, o = O.arena(keys)
+    db = torch.from_numpy(np.concatenate([np.zeros(3, np.uint8), b])).cuda()
+    do = torch.from_numpy((o + 3).astype(np.int64)).cuda()
+    h.contains_dev(device_keys(db.data_ptr(), n, 0, do.data_ptr()), cnt.data_ptr() + 8, out.data_ptr())
+    client.synchronize()
+    cr, pr = ref.contains(b, o, per_key=True)
+    assert cnt[1].item() == cr and np.array_equal(out.cpu().numpy(), pr)
+    h.close()
+    f.delete()
+
+
+def test_golden_sequences_on_gpu(client, fresh):
+    for i, s in enumerate(G["bloom_sequences"]):
+        f = client.getBloomFilter(f"{fresh}-{i}")
+        f.tryInitRaw(s["size"], s["k"])
+        for b in s["batches"]:
+            c, flags = f.addEach([bytes.fromhex(x) for x in b["keys"]])
+            assert c == b["count"] and flags.tolist() == b["new"]
+        c, pres = f.containsEach([bytes.fromhex(x) for x in s["probes"]])
+        assert c == s["contains"] and pres.tolist() == s["present"]
+        assert f.exportBitmap().hex() == s["bitmap"]
+        assert f.count() == s["count"]
+        f.delete()
+
+
+def test_export_import_roundtrip(client, fresh):
+    rng = np.random.default_rng(11)
+    keys = [rng.bytes(20) for _ in range(5000)]
+    f = client.getBloomFilter(fresh)
+    f.tryInit(10000, 0.01)
+    f.add(keys)
+    blob = f.exportBitmap()
+    g = client.getBloomFilter(fresh + "b")
+    g.tryInit(10000, 0.01)
+    g.importBitmap(blob)
+    assert g.contains(keys) == len(keys)
+    assert g.exportBitmap() == blob
+    assert g.count() == f.count()
+    f.delete()
+    g.delete()
+
+
+def test_multi_tenant_parity(client, fresh):
+    rng = np.random.default_rng(12)
+    names = [f"{fresh}-{t}" for t in range(7)]
+    shapes = [(14377587, 10), (729, 5), (9585, 7), (64, 7), (1000, 40), (1 << 20, 3), (100003, 17)]
+    refs = []
+    for n, (m, k) in zip(names, shapes):
+        client.getBloomFilter(n).tryInitRaw(m, k)
+        refs.append(O.OracleBloom(m, k))
+    handles = [BloomHandle(client, n) for n in names]
+    # segments: tenant order with a repeated tenant (sequential semantics across segments)
+    order = [0, 1, 2, 3, 4, 5, 6, 3, 0]
+    sizes = [int(x) for x in rng.integers(1, 400, size=len(order))]
+    keys, segs = [], [0]
+    for t, sz in zip(order, sizes):
+        pool = [rng.bytes(int(L)) for L in rng.integers(0, 40, size=sz // 2 + 1)]
+        keys += [pool[int(j)] for j in rng.integers(0, len(pool), size=sz)]
+        segs.append(len(keys))
+    segs = np.array(segs, np.uint64)
+    counts, flags = bloom_add_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
+    for s, t in enumerate(order):
+        sub = keys[int(segs[s]):int(segs[s + 1])]
+        c, fl = refs[t].add(*O.arena(sub), per_key=True)
+        assert counts[s] == c
+        assert np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl)
+    probes_c, probes_f = bloom_contains_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
+    for s, t in enumerate(order):
+        sub = keys[int(segs[s]):int(segs[s + 1])]
+        c, fl = refs[t].contains(*O.arena(sub), per_key=True)
+        assert probes_c[s] == c and np.array_equal(probes_f[int(segs[s]):int(segs[s + 1])], fl)
+    for n, r in zip(names, refs):
+        assert client.getBloomFilter(n).exportBitmap() == r.redis_string()
+    for h in handles:
+        h.close()
+    for n in names:
+        client.getBloomFilter(n).delete()
+
+
+def test_device_path_matches_host_path(client, fresh):
+    import torch
+
+    rng = np.random.default_rng(13)
+    mat = rng.integers(0, 256, size=(100000, 32), dtype=np.uint8)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 24, 7)
+    h = BloomHandle(client, fresh)
+    d = torch.from_numpy(mat).cuda()
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    from redisson_amd import device_keys
+
+    dk = device_keys(d.data_ptr(), 50000, 32)
+    h.add_dev(dk, cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    dk2 = device_keys(d.data_ptr(), 100000, 32)
+    h.contains_dev(dk2, cnt.data_ptr() + 8, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = O.OracleBloom(1 << 24, 7)
+    ca = ref.add(*O.fixed_arena(mat[:50000]))
+    cc = ref.contains(*O.fixed_arena(mat))
+    assert cnt.tolist() == [ca, cc]
+    h.close()
+    f.delete()
+
+
+def test_full_size_2pow32_property(client, fresh):
+    """C2 geometry (m = 2^32, k = 7) at 4M 32-byte keys: add counts and per-key flags equal the
+    oracle, no false negatives, false-positive rate near theory, bitmap bytes identical."""
+    rng = np.random.default_rng(0x5EED0002)
+    n = 4_000_000
+    mat = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 32, 7)
+    ref = O.OracleBloom(1 << 32, 7)
+    a = Arena.fixed(mat)
+    cg, ng = f.addEach(a)
+    cr, nr = ref.add(*O.fixed_arena(mat), per_key=True)
+    assert cg == cr == n and np.array_equal(ng, nr)
+    assert f.contains(a) == n
+    fresh_keys = Arena.fixed(rng.integers(0, 256, size=(n, 32), dtype=np.uint8))
+    fp = f.contains(fresh_keys)
+    theory = (1 - np.exp(-7 * n / 2**32)) ** 7
+    assert fp <= max(10, 5 * theory * n)
+    assert f.exportBitmap() == ref.redis_string()
+    f.delete()

@@ -1,0 +1,234 @@
+"""RHyperLogLog on the GPU vs the CPU oracle (register-exact, PFCOUNT-integer-exact).
+
+Mirrors T/RedissonHyperLogLogTest.java and the Redis PFADD/PFCOUNT/PFMERGE semantics
+[redis-7.2 hyperloglog.c, restated in oracle/rbx_oracle.c].
+"""
+import base64
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from redisson_amd import Arena, RedisException, hll_add_multi, hll_count_each
+
+pytestmark = pytest.mark.gpu
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+SEED = 0x5EED0000
+
+
+def regs_of(h) -> np.ndarray:
+    d = h.exportDense()
+    assert d[:4] == b"HYLL" and d[4] == 0 and len(d) == 12304
+    return O.hll_dense_unpack(d[16:])
+
+
+# ---- T/RedissonHyperLogLogTest.java ---------------------------------------------------------
+def test_add_all(client, fresh):
+    log = client.getHyperLogLog(fresh)
+    log.addAll([1, 2, 3])
+    assert log.count() == 3
+
+
+def test_add(client, fresh):
+    log = client.getHyperLogLog(fresh)
+    log.add(1)
+    log.add(2)
+    log.add(3)
+    assert log.count() == 3
+
+
+def test_merge(client, fresh):
+    hll1 = client.getHyperLogLog(fresh + "1")
+    assert hll1.add("foo") and hll1.add("bar") and hll1.add("zap") and hll1.add("a")
+    hll2 = client.getHyperLogLog(fresh + "2")
+    assert hll2.add("a") and hll2.add("b") and hll2.add("c") and hll2.add("foo")
+    assert hll2.add("c") is False
+    hll3 = client.getHyperLogLog(fresh + "3")
+    hll3.mergeWith(fresh + "1", fresh + "2")
+    assert hll3.count() == 6
+    assert hll1.countWith(fresh + "2") == 6
+
+
+def test_redis_doc_examples(client, fresh):
+    h = client.getHyperLogLog(fresh)
+    assert h.addAll(["1", "2", "3", "4", "5"]) is True
+    assert h.count() == 5
+    h.addAll(["6", "7", "8", "8", "9", "10"])
+    assert h.count() == 10
+    e = client.getHyperLogLog(fresh + "e")
+    assert e.addAll([]) is True  # PFADD without elements creates the key -> 1
+    assert e.addAll([]) is False
+    assert e.count() == 0
+    assert client.getHyperLogLog(fresh + "missing").count() == 0
+
+
+# ---- register / count parity ------------------------------------------------------------------
+@pytest.mark.parametrize("i", range(8))
+def test_golden_registers_and_counts(client, fresh, i):
+    e = G["hll"][i]
+    n = e["n"]
+    mat = np.random.default_rng(SEED + 4 * 1000003 + n).integers(0, 256, size=(n, 16), dtype=np.uint8)
+    h = client.getHyperLogLog(fresh)
+    h.addAll(Arena.fixed(mat) if n else [])
+    dense = base64.b64decode(e["dense"])
+    assert h.exportDense()[16:] == dense
+    assert h.count() == e["count"]
+
+
+@pytest.mark.parametrize("L", [8, 16, 32, 64, 0])
+def test_parity_element_layouts(client, fresh, L):
+    rng = np.random.default_rng(100 + L)
+    if L:
+        mat = rng.integers(0, 256, size=(200000, L), dtype=np.uint8)
+        a = Arena.fixed(mat)
+        ob, oo = O.fixed_arena(mat)
+    else:
+        elems = [rng.bytes(int(x)) for x in rng.integers(0, 120, size=50000)]
+        a = Arena(elems)
+        ob, oo = O.arena(elems)
+    h = client.getHyperLogLog(fresh)
+    assert h.addAll(a) is True
+    regs = O.hll_new()
+    O.hll_pfadd(regs, ob, oo)
+    assert np.array_equal(regs_of(h), regs)
+    assert h.count() == O.hll_count(regs)
+
+
+def test_pfadd_pipeline_sequential_replies(client, fresh):
+    """A batch of PFADD commands naming the same HLL several times: every reply must see
+    the commands before it (in-order pipeline semantics)."""
+    rng = np.random.default_rng(7)
+    names = [fresh + s for s in ["a", "b", "a", "a", "c", "b", "a"]]
+    pool = [rng.bytes(10) for _ in range(40)]
+    elems, segs = [], [0]
+    for i in range(len(names)):
+        m = int(rng.integers(0, 12))
+        elems += [pool[int(j)] for j in rng.integers(0, 40 if i < 4 else 20, size=m)]
+        segs.append(len(elems))
+    replies = hll_add_multi(client, names, np.array(segs, np.uint64), Arena(elems))
+    refs, want = {}, []
+    for s, nm in enumerate(names):
+        created = nm not in refs
+        r = refs.setdefault(nm, O.hll_new())
+        sub = elems[segs[s]:segs[s + 1]]
+        ch = O.hll_pfadd(r, *O.arena(sub)) if sub else 0
+        want.append(int(bool(ch) or created))
+    assert replies.tolist() == want
+    for nm, r in refs.items():
+        assert np.array_equal(regs_of(client.getHyperLogLog(nm)), r)
+
+
+def test_count_each_and_union(client, fresh):
+    rng = np.random.default_rng(8)
+    names, refs = [], []
+    for i in range(50):
+        n = int(rng.integers(0, 20000))
+        mat = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+        nm = f"{fresh}-{i}"
+        client.getHyperLogLog(nm).addAll(Arena.fixed(mat) if n else [])
+        r = O.hll_new()
+        if n:
+            O.hll_pfadd(r, *O.fixed_arena(mat))
+        names.append(nm)
+        refs.append(r)
+    got = hll_count_each(client, names)
+    assert got.tolist() == [O.hll_count(r) for r in refs]
+    u = O.hll_new()
+    for r in refs[:10]:
+        O.hll_merge(u, r)
+    assert client.getHyperLogLog(names[0]).countWith(*names[1:10]) == O.hll_count(u)
+    client.getHyperLogLog(fresh + "dst").mergeWith(*names[:10])
+    assert np.array_equal(regs_of(client.getHyperLogLog(fresh + "dst")), u)
+
+
+def test_tau_branch_and_high_registers(client, fresh):
+    """Registers equal to 51 (hllTau path, evaluated with glibc pow on the host) and
+    imported dense registers up to 63."""
+    rng = np.random.default_rng(9)
+    for trial in range(20):
+        regs = rng.integers(0, 20, size=16384, dtype=np.uint8)
+        regs[rng.integers(0, 16384, size=int(rng.integers(1, 50)))] = 51
+        if trial % 2:
+            regs[rng.integers(0, 16384, size=5)] = 63
+        s = b"HYLL" + bytes([0, 0, 0, 0]) + bytes([0, 0, 0, 0, 0, 0, 0, 0x80]) + O.hll_dense_pack(regs)
+        h = client.getHyperLogLog(f"{fresh}-{trial}")
+        h.importString(s)
+        assert h.count() == O.hll_count(regs)
+
+
+def test_cached_cardinality_semantics(client, fresh):
+    # a valid cached card in the header is returned as is by PFCOUNT (like redis)
+    regs = O.hll_new()
+    O.hll_pfadd(regs, *O.arena([b"x", b"y"]))
+    s = b"HYLL" + bytes(4) + (1234).to_bytes(8, "little") + O.hll_dense_pack(regs)
+    h = client.getHyperLogLog(fresh)
+    h.importString(s)
+    assert h.count() == 1234
+    assert h.exportDense()[8:16] == (1234).to_bytes(8, "little")
+    h.add(b"z")  # changes a register -> cache invalidated -> recomputed
+    O.hll_pfadd(regs, *O.arena([b"z"]))
+    assert h.count() == O.hll_count(regs)
+
+
+def _sparse_encode(regs: np.ndarray) -> bytes:
+    """Redis sparse encoding (ZERO / XZERO / VAL opcodes) of registers <= 32."""
+    out = bytearray()
+    i = 0
+    while i < 16384:
+        v = int(regs[i])
+        j = i
+        while j < 16384 and regs[j] == v:
+            j += 1
+        run = j - i
+        while run:
+            if v == 0:
+                if run > 64:
+                    r = min(run, 16384)
+                    out += bytes([0x40 | ((r - 1) >> 8), (r - 1) & 0xFF])
+                else:
+                    r = run
+                    out.append((r - 1) & 0x3F)
+            else:
+                r = min(run, 4)
+                out.append(0x80 | ((v - 1) << 2) | (r - 1))
+            run -= r
+        i = j
+    return bytes(out)
+
+
+def test_sparse_import(client, fresh):
+    rng = np.random.default_rng(10)
+    regs = O.hll_new()
+    O.hll_pfadd(regs, *O.fixed_arena(rng.integers(0, 256, size=(300, 16), dtype=np.uint8)))
+    s = b"HYLL" + bytes([1, 0, 0, 0]) + bytes([0] * 7 + [0x80]) + _sparse_encode(regs)
+    h = client.getHyperLogLog(fresh)
+    h.importString(s)
+    assert np.array_equal(regs_of(h), regs)
+    assert h.count() == O.hll_count(regs)
+
+
+def test_invalid_hll_string(client, fresh):
+    with pytest.raises(RedisException):
+        client.getHyperLogLog(fresh).importString(b"HYLX" + bytes(12300))
+    with pytest.raises(RedisException):
+        client.getHyperLogLog(fresh).importString(b"HYLL" + bytes(20))
+
+
+def test_large_batch_accuracy_and_parity(client, fresh):
+    """C4 geometry per HLL (100k 16-byte elements) for 64 HLLs in one PFADD batch."""
+    rng = np.random.default_rng(0x5EED0004)
+    nh, per = 64, 100_000
+    mat = rng.integers(0, 256, size=(nh * per, 16), dtype=np.uint8)
+    names = [f"{fresh}-{i}" for i in range(nh)]
+    segs = np.arange(nh + 1, dtype=np.uint64) * per
+    replies = hll_add_multi(client, names, segs, Arena.fixed(mat))
+    assert replies.all()
+    counts = hll_count_each(client, names)
+    for i in range(0, nh, 8):
+        r = O.hll_new()
+        O.hll_pfadd(r, *O.fixed_arena(mat[i * per:(i + 1) * per]))
+        assert counts[i] == O.hll_count(r)
+        assert np.array_equal(regs_of(client.getHyperLogLog(names[i])), r)
+    assert np.all(np.abs(counts.astype(np.float64) - per) / per < 0.03)

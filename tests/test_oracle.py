@@ -1,0 +1,160 @@
+"""Pins the CPU oracle (oracle/rbx_oracle.c) and cross-checks it against the independent
+pure-Python restatement (oracle/pyref.py).  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import pyref as P
+
+# Upstream google/highwayhash test vectors: key {0x0706050403020100, ...}, input bytes
+# 0,1,...,len-1 (highwayhash/highwayhash_test.cc kExpected64 / kExpected128).  Redisson's
+# HighwayHash.java is the upstream portable Java implementation (finalize128 included).
+KAT_KEY = [0x0706050403020100, 0x0F0E0D0C0B0A0908, 0x1716151413121110, 0x1F1E1D1C1B1A1918]
+KAT64 = [0x907A56DE22C26E53, 0x7EAB43AAC7CDDD78, 0xB8D0569AB0B53D62, 0x5C6BEFAB8A463D80,
+         0xF205A46893007EDA, 0x2B8A1668E4A94541, 0xBD4CCC325BEFCA6F, 0x4D02AE1738F59482,
+         0xE1205108E55F3171, 0x32D2644EC77A1584, 0xF6E10ACDB103A90B, 0xC3BBF4615B415C15]
+KAT128 = [(0x0FED268F9D8FFEC7, 0x33565E767F093E6F), (0xD6B0A8893681E7A8, 0xDC291DF9EB9CDCB4),
+          (0x3D15AD265A16DA04, 0x78085638DC32E868)]
+
+
+@pytest.mark.parametrize("n", range(len(KAT64)))
+def test_highwayhash64_kat(n):
+    d = bytes(range(n))
+    assert O.highway_hash64(d, KAT_KEY) == KAT64[n]
+    assert P.highway_hash64(d, KAT_KEY) == KAT64[n]
+
+
+@pytest.mark.parametrize("n", range(len(KAT128)))
+def test_highwayhash128_kat(n):
+    d = bytes(range(n))
+    assert O.highway_hash128(d, KAT_KEY) == KAT128[n]
+
+
+def test_hash128_c_vs_python_all_tail_shapes():
+    rng = np.random.default_rng(1)
+    for L in range(0, 130):
+        d = rng.bytes(L)
+        assert O.redisson_hash128(d) == P.highway_hash128(d), L
+
+
+def test_murmur64a_smhasher_verification():
+    # SMHasher VerificationTest: keys {0..i-1} hashed with seed 256-i, then the 256
+    # 8-byte hashes hashed with seed 0; low 32 bits == 0x1F0D3804 for MurmurHash64A.
+    key = bytearray(256)
+    hashes = bytearray()
+    for i in range(256):
+        key[i] = i
+        hashes += O.murmur64a(bytes(key[:i]), 256 - i).to_bytes(8, "little")
+    assert O.murmur64a(bytes(hashes), 0) & 0xFFFFFFFF == 0x1F0D3804
+
+
+def test_murmur_c_vs_python():
+    rng = np.random.default_rng(2)
+    for L in range(0, 70):
+        d = rng.bytes(L)
+        assert O.murmur64a(d) == P.murmur64a(d)
+        assert O.hll_patlen(d) == P.hll_patlen(d)
+
+
+def test_crc16_kat_and_slots():
+    assert O.crc16(b"123456789") == 0x31C3  # Redis Cluster spec
+    assert P.crc16(b"123456789") == 0x31C3
+    for k in [b"foo{bar}baz", b"{user1000}.following", b"{}", b"a}b{c}", b"x{}y", b"{a", b""]:
+        assert O.calc_slot(k) == P.calc_slot(k)
+    assert O.calc_slot(b"{user1000}.following") == O.calc_slot(b"{user1000}.followers")
+
+
+def test_bloom_config_kat():
+    # T/RedissonBloomFilterTest.java:69-76
+    assert O.bloom_optimal(100, 0.03) == (729, 5)
+    # BASELINE.md derived parameters
+    assert O.bloom_optimal(10_000_000, 0.01) == (95850583, 7)
+    assert O.bloom_optimal(1_000_000, 1e-3) == (14377587, 10)
+    assert O.bloom_optimal(448_089_842, 0.01) == (4294967293, 7)
+
+
+@pytest.mark.parametrize("n,p", [(1, -1), (1, 2), (1, 1), (10**12, 1e-9)])
+def test_bloom_config_illegal_argument(n, p):
+    # testFalseProbability1/2, testSizeZero (:44-66); size > getMaxSize()
+    with pytest.raises(O.OracleError):
+        O.bloom_optimal(n, p)
+
+
+def test_bloom_indexes_python_vs_c():
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        h1, h2 = int(rng.integers(0, 2**63)) * 2 + 1, int(rng.integers(0, 2**63))
+        for size, k in [(729, 5), (95850583, 7), (2**32, 7), (4294967293, 40)]:
+            assert O.bloom_indexes(h1, h2, k, size) == P.bloom_indexes(h1, h2, k, size)
+
+
+def test_java_math_round():
+    assert O.java_math_round(0.49999999999999994) == 0
+    assert O.java_math_round(0.5) == 1
+    assert O.java_math_round(-0.5) == 0
+    assert O.java_math_round(-1.5) == -1
+    assert O.java_math_round(2.5) == 3
+    assert O.java_math_round(float("inf")) == 2**63 - 1
+    assert O.java_math_round(float("nan")) == 0
+
+
+def _sk(xs):
+    return O.arena([x.encode() for x in xs])
+
+
+def test_redisson_bloom_tests_replay_on_oracle():
+    # T/RedissonBloomFilterTest.java testContainsAll / testAddAll, StringCodec bytes
+    f = O.OracleBloom(*O.bloom_optimal(100, 0.03))
+    assert f.contains(*_sk(["1", "2", "3"])) == 0
+    assert f.add(*_sk(["1", "2", "3"])) == 3
+    assert f.contains(*_sk(["1", "2", "3"])) == 3
+    assert f.contains(*_sk(["1", "5"])) == 1
+    g = O.OracleBloom(*O.bloom_optimal(100, 0.03))
+    assert g.add(*_sk(["1", "2", "3"])) == 3
+    assert g.add(*_sk(["1", "2", "3"])) == 0
+    assert g.count() == 3
+    assert g.add(*_sk(["1", "5"])) == 1
+    assert g.count() == 4
+
+
+def test_empty_collection_is_arithmetic_exception():
+    f = O.OracleBloom(729, 5)
+    assert f.add(*O.arena([])) == -4
+    assert f.contains(*O.arena([])) == -4
+
+
+def test_hll_reference_counts():
+    # T/RedissonHyperLogLogTest.java and the Redis PFADD/PFCOUNT/PFMERGE doc examples
+    def pf(regs, xs):
+        return O.hll_pfadd(regs, *_sk(xs))
+
+    r = O.hll_new()
+    pf(r, ["1", "2", "3"])
+    assert O.hll_count(r) == 3
+    h1, h2 = O.hll_new(), O.hll_new()
+    assert [pf(h1, [x]) for x in ["foo", "bar", "zap", "a"]] == [1, 1, 1, 1]
+    assert [pf(h2, [x]) for x in ["a", "b", "c", "foo", "c"]] == [1, 1, 1, 1, 0]
+    h3 = O.hll_new()
+    O.hll_merge(h3, h1)
+    O.hll_merge(h3, h2)
+    assert O.hll_count(h3) == 6
+    h = O.hll_new()
+    pf(h, ["1", "2", "3", "4", "5"])
+    assert O.hll_count(h) == 5
+    pf(h, ["6", "7", "8", "8", "9", "10"])
+    assert O.hll_count(h) == 10
+    assert O.hll_count(O.hll_new()) == 0
+
+
+def test_hll_dense_pack_roundtrip():
+    rng = np.random.default_rng(5)
+    regs = rng.integers(0, 64, size=16384, dtype=np.uint8)
+    assert np.array_equal(O.hll_dense_unpack(O.hll_dense_pack(regs)), regs)
+
+
+def test_hll_estimator_accuracy():
+    rng = np.random.default_rng(6)
+    for n in (1000, 100000):
+        regs = O.hll_new()
+        O.hll_pfadd(regs, *O.fixed_arena(rng.integers(0, 256, size=(n, 16), dtype=np.uint8)))
+        assert abs(O.hll_count(regs) - n) / n < 0.03
