@@ -144,8 +144,11 @@ def run_c2(args, world, rank, local):
     K = 7
     SIZE = 1 << 32
     n = args.keys
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-null) stream: every engine launch and every timing event goes on it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    assert sptr, "need a non-default stream handle"
     client = RedissonClient(local)
     f = client.getBloomFilter("bench-c2")
     f.tryInitRaw(SIZE, K)
@@ -253,7 +256,8 @@ def run_c4(args, world, rank, local):
     NH = 10_000
     per = max(1, args.keys // NH)  # elements per HLL per GPU per step
     n = NH * per
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     client = RedissonClient(local)
     hs = []

@@ -106,10 +106,24 @@ SIGNATURES = {
 _lib = None
 
 
+def _adopt_torch_runtime() -> None:
+    """One HIP runtime per process.  PyTorch ships its own libamdhip64.so.7 (same SONAME as
+    /opt/rocm/lib's).  Whichever loads first is shared by both, and torch cannot run on a
+    runtime other than its own, so when torch is installed it is loaded before librbx.so
+    and librbx.so binds to torch's runtime.  (Without torch, /opt/rocm/lib is used.)"""
+    import importlib.util
+
+    if os.environ.get("RBX_NO_TORCH_RUNTIME") == "1":
+        return
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def lib() -> C.CDLL:
     """Loads librbx.so (built in-tree by __graft_entry__.build()).  Fails loudly."""
     global _lib
     if _lib is None:
+        _adopt_torch_runtime()
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build the HIP engine first "
