@@ -39,7 +39,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
-    p.add_argument("--keys", type=int, default=100_000_000, help="keys per step per GPU (C2)")
+    p.add_argument("--keys", type=int, default=100_000_000, help="keys (C2/C3) or elements (C4) per step per GPU")
+    p.add_argument("--tenants", type=int, default=100_000, help="C3 tenant count (whole node)")
+    p.add_argument("--elements", type=int, default=1_000_000_000, help="C4 PFADD elements per step per GPU")
+    p.add_argument("--stage1", type=int, default=None, help="contains early-exit schedule (rbx_tune)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -230,13 +233,100 @@ def run_c2(args, world, rank, local):
                    "parallelism": f"replicas x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes_per_launch": algo_bytes, "kernel": "k_bloom_contains<32,8>",
+                     "algorithmic_bytes_per_launch": algo_bytes, "kernel": "k_bloom_contains<32,8,4>",
                      "kernel_avg_ms": kern_ms,
+                     # north-star definition: keys/s x k / measured random-gather peak at this
+                     # working set (> 1 is possible: early exit skips gathers of absent keys)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
         "extra": {"add_keys_per_s_per_gpu": half / (add_ms / 1e3), "add_new_keys": n_new,
                   "present_per_step": total_present // args.steps, "wall_s_timed": wall},
     }
     h.close()
+    client.shutdown()
+    return res
+
+
+# ------------------------------------------------------------------------------------------
+# C3: 100k tenant filters tryInit(1e6, 1e-3), sharded by CRC16 slot across the node's GPUs
+# ------------------------------------------------------------------------------------------
+def run_c3(args, world, rank, local):
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from redisson_amd import BloomHandle, RedissonClient, calc_slot, device_keys, slot_to_gpu
+    from redisson_amd import _lib as L
+
+    NT = args.tenants
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+    client = RedissonClient(local)
+    names = [f"tenant:{t:06d}" for t in range(NT)]
+    mine = [nm for nm in names if slot_to_gpu(calc_slot(nm), world) == rank]
+    nt = len(mine)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0003 + rank)
+    # a pool of random bytes: each bit set with p = 1/2 = the fill of a filter at its design
+    # load (1 - exp(-k n / m) = 0.50 for n = 1e6, m = 14,377,587, k = 10)
+    pool = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+    t0 = time.perf_counter()
+    handles = []
+    rng = np.random.default_rng(rank)
+    for nm in mine:
+        f = client.getBloomFilter(nm)
+        f.tryInit(1_000_000, 1e-3)
+        nbytes = (f._size + 7) // 8
+        off = int(rng.integers(0, (pool.numel() - nbytes) // 256)) * 256
+        assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), pool.data_ptr() + off, nbytes, sptr) == 0
+        handles.append(BloomHandle(client, nm))
+    setup_s = time.perf_counter() - t0
+    size, k = handles[0].size, handles[0].k
+    per = max(1, args.keys // nt)
+    n = per * nt
+    keys = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    seg = torch.arange(nt + 1, dtype=torch.int64, device="cuda") * per
+    counts = torch.zeros(nt, dtype=torch.int64, device="cuda")
+    arr = (C.c_void_p * nt)(*[h.h.value for h in handles])
+    dk = device_keys(keys.data_ptr(), n, 16)
+
+    def step():
+        assert L.lib().rbx_bloom_contains_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
+                                                     counts.data_ptr(), sptr) == 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    step_s = max_over_ranks(world, ms / 1e3)
+    value = sum_over_ranks(world, n) / step_s
+    present = int(counts.sum().item()) / max(args.warmup + args.steps, 1)
+    algo = n * (16 + k * 8)
+    achieved = algo / (ms / 1e3) / 1e9
+    res = {
+        "metric": "Bloom contains keys/sec (whole node), C3: 100k tenant filters tryInit(1e6,1e-3), CRC16-slot sharded",
+        "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C3 one contains(Collection) per tenant, {per} random 16-byte keys each, "
+                               f"{nt} of {NT} tenants on this GPU (slot*N/16384), filters at design fill 0.5",
+                   "tenants_total": NT, "tenants_this_gpu": nt, "size_bits": size, "k": k, "keys_per_gpu": n,
+                   "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, "k_bloom_contains_multi"),
+                     "kernel": "k_bloom_contains_multi<16,16,4>", "kernel_avg_ms": ms},
+        "extra": {"setup_s": setup_s, "present_fraction": present / n},
+    }
+    for h in handles:
+        h.close()
     client.shutdown()
     return res
 
@@ -254,7 +344,7 @@ def run_c4(args, world, rank, local):
     from redisson_amd import _lib as L
 
     NH = 10_000
-    per = max(1, args.keys // NH)  # elements per HLL per GPU per step
+    per = max(1, args.elements // NH)  # elements per HLL per GPU per step
     n = NH * per
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -285,6 +375,24 @@ def run_c4(args, world, rank, local):
     e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.steps
+    merge_ms = None
+    if world > 1:  # element-partitioned registers -> RCCL uint8 max all-reduce over xGMI
+        import torch.distributed as dist
+
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            assert L.lib().rbx_rccl_unique_id(uid) == 0
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_uint8 * 128).from_buffer_copy(obj[0])
+        assert L.lib().rbx_rccl_init(client.ctx, uid, world, rank) == 0
+        assert L.lib().rbx_hll_allreduce_max(client.ctx, arr, NH) == 0  # warm
+        L.lib().rbx_synchronize(client.ctx)
+        barrier(world)
+        t0 = time.perf_counter()
+        assert L.lib().rbx_hll_allreduce_max(client.ctx, arr, NH) == 0
+        L.lib().rbx_synchronize(client.ctx)
+        merge_ms = (time.perf_counter() - t0) * 1e3
     out = np.zeros(NH, np.uint64)
     t0 = time.perf_counter()
     assert L.lib().rbx_hll_count_each_handles(client.ctx, arr, NH, out.ctypes.data_as(L.u64p)) == 0
@@ -302,7 +410,8 @@ def run_c4(args, world, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, "k_hll_pfadd"),
                      "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms},
-        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean())},
+        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean()), "rccl_max_allreduce_ms": merge_ms,
+                  "allreduce_bytes": NH * 16384},
     }
     for hp in hs:
         L.lib().rbx_hll_close(hp)
@@ -313,6 +422,10 @@ def run_c4(args, world, rank, local):
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
+    if args.stage1 is not None:
+        from redisson_amd import _lib as L
+
+        assert L.lib().rbx_tune(b"contains_stage1", args.stage1) == 0
     log(f"[bench] rank {rank}/{world} workload {args.workload}")
     if args.workload == "c2":
         res = run_c2(args, world, rank, local)
@@ -321,7 +434,7 @@ def main():
     elif args.workload == "c4":
         res = run_c4(args, world, rank, local)
     else:
-        raise SystemExit("c3 bench: see DESIGN.md (round 2)")
+        res = run_c3(args, world, rank, local)
     if rank == 0:
         res.setdefault("cpu_baseline", None)
         print(json.dumps(res), flush=True)

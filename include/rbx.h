@@ -122,6 +122,9 @@ int rbx_bloom_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap,
 /* SET name <bytes>: replaces the bitmap string (warm start from Redis data). */
 int rbx_bloom_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint64_t len);
 
+/* SET name from a DEVICE buffer (device-resident snapshot restore); synchronous. */
+int rbx_bloom_import_dev(rbx_ctx *ctx, const char *name, const uint8_t *d_bytes, uint64_t len, void *stream);
+
 /* ---- Bloom handles and the device-resident batch path ------------------------------ */
 int rbx_bloom_open(rbx_ctx *ctx, const char *name, rbx_bloom **out);
 int rbx_bloom_close(rbx_bloom *b);

@@ -70,6 +70,7 @@ SIGNATURES = {
     "rbx_bloom_renamenx": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_int)]),
     "rbx_bloom_export": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64, u64p]),
     "rbx_bloom_import": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64]),
+    "rbx_bloom_import_dev": (C.c_int, [vp, C.c_char_p, vp, C.c_uint64, vp]),
     "rbx_bloom_open": (C.c_int, [vp, C.c_char_p, C.POINTER(vp)]),
     "rbx_bloom_close": (C.c_int, [vp]),
     "rbx_bloom_handle_config": (C.c_int, [vp, u64p, u32p]),
@@ -97,6 +98,7 @@ SIGNATURES = {
     "rbx_rccl_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
     "rbx_hll_allreduce_max": (C.c_int, [vp, C.POINTER(vp), C.c_uint32]),
     "rbx_bench_gather": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, vp]),
+    "rbx_tune": (C.c_int, [C.c_char_p, C.c_int]),
     # include/rbx_selftest.h
     "rbx_selftest_mod": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "rbx_selftest_hash128": (None, [u8p, C.c_uint64, u64p]),

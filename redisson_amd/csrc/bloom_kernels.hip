@@ -90,32 +90,67 @@ __device__ __forceinline__ void wave_seg_add(bool active, uint32_t seg, uint32_t
 // ---------------------------------------------------------------------------------
 // contains
 // ---------------------------------------------------------------------------------
-// Tests the k bits of one key; KMAX >= k unrolled so all k loads issue before use.
-template <int KMAX>
+// Loads bits [J0, J1) of the key (h already advanced to hash J0) and returns their AND.
+template <int J0, int J1>
+__device__ __forceinline__ bool probe_range(const uint32_t *__restrict__ bm, const ModParams &mp, uint32_t k,
+                                            uint64_t &h, uint64_t h1, uint64_t h2) {
+    uint32_t word[J1 - J0], mask[J1 - J0];
+#pragma unroll
+    for (int j = J0; j < J1; ++j) {
+        if ((uint32_t)j < k) {
+            const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
+            word[j - J0] = bm[idx >> 5];
+            mask[j - J0] = bit_in_word(idx);
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    bool all = true;
+#pragma unroll
+    for (int j = J0; j < J1; ++j)
+        if ((uint32_t)j < k) all &= (word[j - J0] & mask[j - J0]) != 0u;
+    return all;
+}
+
+// Tests the k bits of one key (KMAX >= k, unrolled).  All loads of a stage issue before any
+// is used.  A key is absent as soon as one bit is 0, so later stages run only while every
+// bit so far is set (early exit; the result is identical).  Schedules (SCHED):
+//   0: one stage of k loads          1: 1, then k-1        2: 2, then k-2
+//   3: 3, then k-3                   4: doubling 1, 2, 4, 8 ...
+// On a filter with fill f an absent key costs ~1 + (k-1) f gathers under schedule 1 and
+// ~1 + 2f + 4f^3 under schedule 4 (the better one when f is large, e.g. 0.5 at design load).
+template <int KMAX, int SCHED = 0>
 __device__ __forceinline__ bool probe_all_set(const uint32_t *__restrict__ bm, const ModParams &mp,
                                               uint32_t k, uint64_t h1, uint64_t h2) {
     if constexpr (KMAX > 0) {
-        uint32_t word[KMAX], mask[KMAX];
         uint64_t h = h1;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            if ((uint32_t)j < k) {
-                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
-                word[j] = bm[idx >> 5];
-                mask[j] = bit_in_word(idx);
+        if constexpr (SCHED == 0 || KMAX <= 1) {
+            return probe_range<0, KMAX>(bm, mp, k, h, h1, h2);
+        } else if constexpr (SCHED >= 1 && SCHED <= 3) {
+            constexpr int S = SCHED < KMAX ? SCHED : KMAX;
+            if (!probe_range<0, S>(bm, mp, k, h, h1, h2)) return false;
+            if (k <= (uint32_t)S) return true;
+            return probe_range<S, KMAX>(bm, mp, k, h, h1, h2);
+        } else {  // doubling
+            if (!probe_range<0, 1>(bm, mp, k, h, h1, h2)) return false;
+            if (k <= 1) return true;
+            if constexpr (KMAX > 1) {
+                constexpr int E2 = KMAX < 3 ? KMAX : 3;
+                if (!probe_range<1, E2>(bm, mp, k, h, h1, h2)) return false;
+                if (k <= (uint32_t)E2) return true;
             }
-            h += (j & 1) ? h1 : h2;
+            if constexpr (KMAX > 3) {
+                constexpr int E3 = KMAX < 7 ? KMAX : 7;
+                if (!probe_range<3, E3>(bm, mp, k, h, h1, h2)) return false;
+                if (k <= (uint32_t)E3) return true;
+            }
+            if constexpr (KMAX > 7) return probe_range<7, KMAX>(bm, mp, k, h, h1, h2);
+            return true;
         }
-        bool all = true;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if ((uint32_t)j < k) all &= (word[j] & mask[j]) != 0u;
-        return all;
     } else {
-        // any k: 8 loads in flight per round
+        // any k: 8 loads in flight per round, stop after the first round with a zero bit
         bool all = true;
         uint64_t h = h1;
-        for (uint32_t j0 = 0; j0 < k; j0 += 8) {
+        for (uint32_t j0 = 0; j0 < k && all; j0 += 8) {
             uint32_t word[8], mask[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -135,7 +170,7 @@ __device__ __forceinline__ bool probe_all_set(const uint32_t *__restrict__ bm, c
     }
 }
 
-template <int KLEN, int KMAX>
+template <int KLEN, int KMAX, int S1>
 __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint32_t *__restrict__ bm,
                                                         ModParams mp, uint32_t k,
                                                         uint8_t *__restrict__ out,
@@ -145,7 +180,7 @@ __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < keys.n; i += stride) {
         uint64_t h1, h2;
         hash_key<KLEN>(keys, i, h1, h2);
-        const bool p = probe_all_set<KMAX>(bm, mp, k, h1, h2);
+        const bool p = probe_all_set<KMAX, S1>(bm, mp, k, h1, h2);
         if (out) out[i] = p;
         present += p;
     }
@@ -166,7 +201,7 @@ __device__ __forceinline__ uint32_t upper_seg(const uint64_t *off, uint32_t nseg
     return lo;
 }
 
-template <int KLEN, int KMAX>
+template <int KLEN, int KMAX, int S1>
 __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, const FilterDesc *__restrict__ filt,
                                                               const uint64_t *__restrict__ seg_off, uint32_t nseg,
                                                               uint8_t *__restrict__ out,
@@ -199,7 +234,7 @@ __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, cons
             const FilterDesc f = filt[seg];
             uint64_t h1, h2;
             hash_key<KLEN>(keys, i, h1, h2);
-            p = probe_all_set<KMAX>(f.bm, f.mp, f.k, h1, h2);
+            p = probe_all_set<KMAX, S1>(f.bm, f.mp, f.k, h1, h2);
             if (out) out[i] = p;
         }
         if (counts) wave_seg_add(active, seg, p, counts);
@@ -441,12 +476,35 @@ static inline unsigned grid_for(uint64_t n, unsigned cap) {
     return (unsigned)(g < cap ? g : cap);
 }
 
+// Early-exit width for contains (rbx_tune("contains_stage1", n)); 0 disables.
+static int g_stage1 = 4;
+void set_contains_stage1(int v) { g_stage1 = v; }
+int get_contains_stage1() { return g_stage1; }
+
+template <int KLEN, int KMAX, int S1>
+static void launch_contains_s(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+}
+
+template <int KLEN, int KMAX>
+static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
+                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    switch (g_stage1) {
+    case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid); break;
+    case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid); break;
+    case 3: launch_contains_s<KLEN, KMAX, 3>(keys, bm, mp, k, out, count, st, grid); break;
+    case 4: launch_contains_s<KLEN, KMAX, 4>(keys, bm, mp, k, out, count, st, grid); break;
+    default: launch_contains_s<KLEN, KMAX, 1>(keys, bm, mp, k, out, count, st, grid); break;
+    }
+}
+
 template <int KLEN>
 static void launch_contains_k(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
-    if (k <= 8) hipLaunchKernelGGL((k_bloom_contains<KLEN, 8>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
-    else if (k <= 16) hipLaunchKernelGGL((k_bloom_contains<KLEN, 16>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
-    else hipLaunchKernelGGL((k_bloom_contains<KLEN, 0>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+    if (k <= 8) launch_contains_km<KLEN, 8>(keys, bm, mp, k, out, count, st, grid);
+    else if (k <= 16) launch_contains_km<KLEN, 16>(keys, bm, mp, k, out, count, st, grid);
+    else launch_contains_s<KLEN, 0, 0>(keys, bm, mp, k, out, count, st, grid);
 }
 
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
@@ -464,9 +522,15 @@ template <int KLEN>
 static void launch_contains_multi_k(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off,
                                     uint32_t nseg, uint32_t kmax, uint8_t *out, unsigned long long *counts,
                                     hipStream_t st, unsigned grid) {
-    if (kmax <= 8) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
-    else if (kmax <= 16) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
-    else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 0>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    const bool dbl = g_stage1 == 4;
+    if (kmax <= 8) {
+        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    } else if (kmax <= 16) {
+        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    }
+    else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 0, 0>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
 }
 
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,

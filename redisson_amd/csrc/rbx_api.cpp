@@ -85,12 +85,55 @@ struct BloomConfig {
     std::string fpp_str;
 };
 
+// Small bitmaps (<= 64 MiB) come from 1 GiB slabs, exact-size free lists, so that
+// 100k tenant filters do not cost 100k hipMalloc calls; large ones get their own buffer.
+struct SlabPool {
+    std::mutex mu;
+    std::vector<void *> slabs;
+    std::map<uint64_t, std::vector<void *>> free_by_size;
+    uint8_t *cur = nullptr;
+    uint64_t left = 0;
+    static constexpr uint64_t kSlab = 1ull << 30, kMaxSmall = 64ull << 20;
+    void *get(uint64_t bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        auto &fl = free_by_size[bytes];
+        if (!fl.empty()) {
+            void *p = fl.back();
+            fl.pop_back();
+            return p;
+        }
+        if (left < bytes) {
+            void *s = nullptr;
+            if (hipMalloc(&s, kSlab) != hipSuccess) return nullptr;
+            slabs.push_back(s);
+            cur = (uint8_t *)s;
+            left = kSlab;
+        }
+        void *p = cur;
+        cur += bytes;
+        left -= bytes;
+        return p;
+    }
+    void put(void *p, uint64_t bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        free_by_size[bytes].push_back(p);
+    }
+    ~SlabPool() {
+        for (void *s : slabs) (void)hipFree(s);
+    }
+};
+
 struct Bitmap {  // a Redis string used with SETBIT/GETBIT
     int device = 0;
     uint32_t *d_words = nullptr;
     uint64_t cap_bytes = 0;                 // allocated bytes (multiple of 256)
-    unsigned long long *d_len = nullptr;    // device word: Redis string length
+    unsigned long long *d_len = nullptr;    // device word: Redis string length (in the slab too)
+    std::shared_ptr<SlabPool> pool;         // set when d_words/d_len came from the pool
     ~Bitmap() {
+        if (pool) {
+            pool->put(d_words, cap_bytes + 256);
+            return;
+        }
         if (d_words) (void)hipFree(d_words);
         if (d_len) (void)hipFree(d_len);
     }
@@ -143,6 +186,8 @@ struct rbx_ctx {
     std::vector<FilterDesc> filt_cache;  // content of filt_table
     uint64_t filt_generation = 0;
     uint64_t generation = 1;  // bumped whenever a bitmap is (re)allocated or freed
+
+    std::shared_ptr<SlabPool> slab = std::make_shared<SlabPool>();
 
     // HLL register pool: chunks of kHllPerChunk x 16 KiB
     std::vector<uint8_t *> hll_chunks;
@@ -298,8 +343,16 @@ static int new_bitmap(rbx_ctx *c, uint64_t size_bits, std::shared_ptr<Bitmap> *o
     b->device = c->device;
     uint64_t bytes = ((size_bits + 7) / 8 + 255) & ~255ULL;
     if (bytes == 0) bytes = 256;
-    HIP_TRY(hipMalloc(&b->d_words, bytes));
-    HIP_TRY(hipMalloc(&b->d_len, sizeof(unsigned long long)));
+    if (bytes <= SlabPool::kMaxSmall) {  // words + a 256-byte tail holding the length word
+        uint8_t *p = (uint8_t *)c->slab->get(bytes + 256);
+        if (!p) return fail(RBX_E_OOM, "bitmap slab allocation failed");
+        b->pool = c->slab;
+        b->d_words = (uint32_t *)p;
+        b->d_len = (unsigned long long *)(p + bytes);
+    } else {
+        HIP_TRY(hipMalloc(&b->d_words, bytes));
+        HIP_TRY(hipMalloc(&b->d_len, sizeof(unsigned long long)));
+    }
     HIP_TRY(hipMemsetAsync(b->d_words, 0, bytes, c->stream));
     HIP_TRY(hipMemsetAsync(b->d_len, 0, sizeof(unsigned long long), c->stream));
     b->cap_bytes = bytes;
@@ -311,13 +364,24 @@ static int new_bitmap(rbx_ctx *c, uint64_t size_bits, std::shared_ptr<Bitmap> *o
 static int grow_bitmap(rbx_ctx *c, Bitmap &b, uint64_t size_bits) {
     uint64_t bytes = ((size_bits + 7) / 8 + 255) & ~255ULL;
     if (bytes <= b.cap_bytes) return RBX_OK;
+    // always move to a dedicated allocation (words + length word)
     uint32_t *nw = nullptr;
+    unsigned long long *nl = nullptr;
     HIP_TRY(hipMalloc(&nw, bytes));
+    HIP_TRY(hipMalloc(&nl, sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(nw, 0, bytes, c->stream));
     HIP_TRY(hipMemcpyAsync(nw, b.d_words, b.cap_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(nl, b.d_len, sizeof(unsigned long long), hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipFree(b.d_words));
+    if (b.pool) {
+        b.pool->put(b.d_words, b.cap_bytes + 256);
+        b.pool.reset();
+    } else {
+        HIP_TRY(hipFree(b.d_words));
+        HIP_TRY(hipFree(b.d_len));
+    }
     b.d_words = nw;
+    b.d_len = nl;
     b.cap_bytes = bytes;
     c->generation++;
     return RBX_OK;
@@ -865,6 +929,34 @@ int rbx_bloom_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_
     unsigned long long L = len;
     HIP_TRY(hipMemcpyAsync(b->d_len, &L, 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->ks[name] = Entry{KType::Bitmap, nullptr, b, nullptr};
+    return RBX_OK;
+}
+
+// SET name <len bytes from a device buffer> (device-resident snapshot restore)
+int rbx_bloom_import_dev(rbx_ctx *c, const char *name, const uint8_t *d_bytes, uint64_t len, void *stream) {
+    if (!c || !name || (len && !d_bytes)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    if (len > (1ULL << 29)) return fail(RBX_E_ILLEGAL_ARGUMENT, "string exceeds the 512 MiB Redis limit");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    hipStream_t st = pick_stream(c, stream);
+    uint64_t bits = len * 8;
+    Entry *cfg = find(c, config_name(name));
+    if (cfg && cfg->type == KType::Config) bits = std::max<uint64_t>(bits, cfg->cfg->size);
+    std::shared_ptr<Bitmap> b;
+    Entry *e = find(c, name);
+    if (e && e->type == KType::Bitmap && e->bm->cap_bytes >= ((bits + 7) / 8)) {
+        b = e->bm;  // reuse in place (open handles keep seeing it)
+        HIP_TRY(hipMemsetAsync(b->d_words, 0, b->cap_bytes, st));
+    } else {
+        RBX_TRY(new_bitmap(c, bits, &b));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (len) HIP_TRY(hipMemcpyAsync(b->d_words, d_bytes, len, hipMemcpyDeviceToDevice, st));
+    static thread_local unsigned long long L;
+    L = len;
+    HIP_TRY(hipMemcpyAsync(b->d_len, &L, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
     c->ks[name] = Entry{KType::Bitmap, nullptr, b, nullptr};
     return RBX_OK;
 }
@@ -1580,6 +1672,17 @@ int rbx_bench_gather(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint
                         pick_stream(c, stream));
     HIP_TRY(hipGetLastError());
     return RBX_OK;
+}
+
+// Tuning knobs (process-wide).  "contains_stage1": early-exit width of contains (0 = off).
+int rbx_tune(const char *key, int value) {
+    if (!key) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key");
+    if (!strcmp(key, "contains_stage1")) {
+        if (value < 0 || value > 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1 in [0, 4]");
+        set_contains_stage1(value);
+        return RBX_OK;
+    }
+    return fail(RBX_E_ILLEGAL_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
 // Java BigDecimal.valueOf(d).toPlainString() as stored in the config hash.

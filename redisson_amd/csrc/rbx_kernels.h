@@ -59,6 +59,9 @@ void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *
 void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
                          hipStream_t st);
 
+void set_contains_stage1(int v);
+int get_contains_stage1();
+
 // hll_kernels.hip
 struct HllSeg {
     uint8_t *regs;      // 16384 u8 registers

@@ -376,3 +376,73 @@ def test_full_size_2pow32_property(client, fresh):
     assert fp <= max(10, 5 * theory * n)
     assert f.exportBitmap() == ref.redis_string()
     f.delete()
+
+
+def test_import_dev_many_tenants_parity(client, fresh):
+    """Slab-allocated tenant bitmaps loaded from a device buffer (SET from device memory),
+    then one multi-tenant contains batch checked per key against the oracle."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    nt = 300
+    names = [f"{fresh}-{i}" for i in range(nt)]
+    pool = rng.integers(0, 256, size=(1 << 22), dtype=np.uint8)
+    dpool = torch.from_numpy(pool).cuda()
+    refs = []
+    from redisson_amd import _lib as L
+
+    for i, nm in enumerate(names):
+        f = client.getBloomFilter(nm)
+        f.tryInit(10000, 0.01)
+        nb = (f.getSize() + 7) // 8
+        off = int(rng.integers(0, (pool.size - nb) // 256)) * 256
+        assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), dpool.data_ptr() + off, nb, None) == 0
+        r = O.OracleBloom(f.getSize(), f.getHashIterations())
+        r.bitmap[:nb] = pool[off:off + nb]
+        r.redis_len = nb
+        refs.append(r)
+        if i % 50 == 0:
+            assert f.exportBitmap() == pool[off:off + nb].tobytes()
+    handles = [BloomHandle(client, nm) for nm in names]
+    per = [int(x) for x in rng.integers(1, 60, size=nt)]
+    keys, segs = [], [0]
+    for p in per:
+        keys += [rng.bytes(16) for _ in range(p)]
+        segs.append(len(keys))
+    segs = np.array(segs, np.uint64)
+    counts, flags = bloom_contains_multi(client, handles, segs, Arena(keys), per_key=True)
+    for s in range(nt):
+        sub = keys[int(segs[s]):int(segs[s + 1])]
+        c, fl = refs[s].contains(*O.arena(sub), per_key=True)
+        assert counts[s] == c and np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl)
+    for h in handles:
+        h.close()
+    for nm in names:  # free-list reuse afterwards
+        client.getBloomFilter(nm).delete()
+    f = client.getBloomFilter(fresh + "again")
+    f.tryInit(10000, 0.01)
+    assert f.add(["x", "y"]) == 2 and f.contains(["x", "y", "z"]) >= 2
+    f.delete()
+
+
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4])
+def test_contains_schedules_identical(client, fresh, sched):
+    """Every early-exit schedule returns exactly the oracle's per-key answers."""
+    from redisson_amd import _lib as L
+
+    rng = np.random.default_rng(31)
+    for size, k in [(14377587, 10), (95850583, 7), (4099, 7), (100003, 13)]:
+        mat = rng.integers(0, 256, size=(60000, 16), dtype=np.uint8)
+        f = client.getBloomFilter(f"{fresh}-{size}")
+        f.tryInitRaw(size, k)
+        ref = O.OracleBloom(size, k)
+        f.add(Arena.fixed(mat[:30000]))
+        ref.add(*O.fixed_arena(mat[:30000]))
+        assert L.lib().rbx_tune(b"contains_stage1", sched) == 0
+        try:
+            cg, pg = f.containsEach(Arena.fixed(mat))
+        finally:
+            L.lib().rbx_tune(b"contains_stage1", 4)
+        cr, pr = ref.contains(*O.fixed_arena(mat), per_key=True)
+        assert cg == cr and np.array_equal(pg, pr)
+        f.delete()

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Microbenchmarks on one MI355X (run through gpurun).
+
+  gather  : random 4-byte gather rate vs working-set size (the Bloom roofline)
+  stage1  : contains early-exit width A/B, interleaved rounds in one process
+  sizes   : contains throughput vs filter size (C1 12 MB, C3 1.8 MB, C2 512 MiB)
+  add     : add throughput
+Prints one JSON object per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from redisson_amd import BloomHandle, RedissonClient, device_keys  # noqa: E402
+from redisson_amd import _lib as L  # noqa: E402
+
+
+def timed(stream, fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="*", default=["gather", "stage1", "sizes", "add"])
+    ap.add_argument("--keys", type=int, default=100_000_000)
+    a = ap.parse_args()
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    client = RedissonClient(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    n = a.keys
+    keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    if "gather" in a.what:
+        for mb in [2, 8, 32, 64, 128, 192, 256, 384, 512, 1024, 4096, 16384]:
+            tb = torch.empty(mb << 20, dtype=torch.uint8, device="cuda")
+            tb.random_(0, 255, generator=g)
+            f = lambda: L.lib().rbx_bench_gather(client.ctx, tb.data_ptr(), tb.numel(), n, 7, sink.data_ptr(), sp)
+            f()
+            ms = timed(stream, f, 3)
+            print(json.dumps({"bench": "gather", "table_MiB": mb, "ms": ms, "gathers_per_s": n * 7 / (ms / 1e3)}),
+                  flush=True)
+            del tb
+
+    if "stage1" in a.what or "sizes" in a.what:
+        cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+        plan = []
+        if "stage1" in a.what:
+            plan.append(("C2_2^32", 1 << 32, 7, [0, 1, 2, 4]))
+        if "sizes" in a.what:
+            plan += [("C1", 95850583, 7, [1, 4]), ("C3", 14377587, 10, [1, 4]), ("C2_twin", 4294967293, 7, [1, 4])]
+        for name, size, k, s1s in plan:
+            fb = client.getBloomFilter("mb-" + name)
+            fb.tryInitRaw(size, k)
+            h = BloomHandle(client, "mb-" + name)
+            # fill to the design load: n_add keys so that fill matches (C2: 50M; C1: 10M; C3: 1M)
+            n_add = {"C2_2^32": n // 2, "C2_twin": n // 2, "C1": 10_000_000, "C3": 1_000_000}[name]
+            h.add_dev(device_keys(keys.data_ptr(), n_add, 32), cnt.data_ptr(), stream=sp)
+            torch.cuda.synchronize()
+            dk = device_keys(keys.data_ptr(), n, 32)
+            res = {}
+            for s1 in s1s:
+                res[s1] = []
+            for rnd in range(5):
+                for s1 in res:
+                    L.lib().rbx_tune(b"contains_stage1", s1)
+                    res[s1].append(timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 8, stream=sp), 2))
+            for s1, v in res.items():
+                med = statistics.median(v)
+                print(json.dumps({"bench": "contains", "filter": name, "size": size, "k": k, "n_added": n_add,
+                                  "stage1": s1, "ms_median": med, "ms_min": min(v),
+                                  "keys_per_s": n / (med / 1e3)}), flush=True)
+            L.lib().rbx_tune(b"contains_stage1", 4)
+            h.close()
+            fb.delete()
+
+    if "add" in a.what:
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        for name, size, k in [("C2_2^32", 1 << 32, 7), ("C1", 95850583, 7)]:
+            fb = client.getBloomFilter("ad-" + name)
+            fb.tryInitRaw(size, k)
+            h = BloomHandle(client, "ad-" + name)
+            m = n // 2
+            ms = timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(), stream=sp), 1)
+            print(json.dumps({"bench": "add", "filter": name, "keys": m, "ms": ms, "keys_per_s": m / (ms / 1e3)}),
+                  flush=True)
+            h.close()
+            fb.delete()
+    client.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic per launch from rocprofv3 --pmc CSVs -> profiles/traffic.json.
+
+Usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> [<hit_pass_dir>] -o profiles/traffic.json
+
+Follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB, collected in
+separate passes; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
+streaming read, so it is doubled ("x2 correction").  For these kernels most fetches are
+random 4-byte gathers (one 64-byte request each, uncalibrated width) -- the uncorrected
+figure is kept beside the corrected one and both are per launch, averaged over launches.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+SHORT = [("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains", r"k_bloom_contains<"),
+         ("k_bloom_add_probe", r"k_bloom_add_probe"), ("k_bloom_add_commit", r"k_bloom_add_commit"),
+         ("k_gather_probe", r"k_gather_probe"), ("k_hll_pfadd", r"k_hll_pfadd"), ("k_hll_count", r"k_hll_count"),
+         ("k_bitcount", r"k_bitcount")]
+
+
+def short(name: str) -> str | None:
+    for s, pat in SHORT:
+        if re.search(pat, name):
+            return s
+    return None
+
+
+def load(d: str):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(p)):
+            s = short(r["Kernel_Name"])
+            if s:
+                agg[s][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("-o", default="profiles/traffic.json")
+    a = ap.parse_args()
+    merged = collections.defaultdict(dict)
+    for d in a.dirs:
+        for k, cs in load(d).items():
+            for c, v in cs.items():
+                merged[k][c] = sum(v) / len(v)
+    out = {}
+    for k, cs in merged.items():
+        fetch = cs.get("FETCH_SIZE")
+        write = cs.get("WRITE_SIZE")
+        e = {"counters_avg_per_launch": cs}
+        if fetch is not None:
+            e["fetch_bytes_uncorrected"] = fetch * 1024
+            e["fetch_bytes_x2"] = 2 * fetch * 1024
+        if write is not None:
+            e["write_bytes"] = write * 1024
+        if fetch is not None:
+            e["hbm_bytes_per_launch"] = 2 * fetch * 1024 + (write or 0) * 1024
+            e["correction"] = "FETCH_SIZE KiB x1024 x2 (gfx950 half-count) + WRITE_SIZE KiB x1024"
+        if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
+            t = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
+            e["tcc_hit_rate"] = cs["TCC_HIT_sum"] / t if t else None
+        out[k] = e
+    os.makedirs(os.path.dirname(a.o) or ".", exist_ok=True)
+    with open(a.o, "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()
