@@ -72,13 +72,20 @@ def barrier(world):
         dist.barrier()
 
 
+def _coll_device():
+    import torch.distributed as dist
+
+    return "cpu" if dist.get_backend() == "gloo" else "cuda"
+
+
 def max_over_ranks(world, v: float) -> float:
+    """The job's step time is the slowest rank's."""
     if world == 1:
         return v
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -89,7 +96,7 @@ def sum_over_ranks(world, v: int) -> int:
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([v], dtype=torch.int64, device="cuda")
+    t = torch.tensor([v], dtype=torch.int64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
 

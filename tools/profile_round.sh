@@ -15,4 +15,11 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o p -- python3 $B > "$OUT/pmc_write.log" 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmc_tcc" -o p -- python3 $B > "$OUT/pmc_tcc.log" 2>&1 || exit 1
 python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" -o "$OUT/traffic.json" > /dev/null || exit 1
+# keep summaries only (gpurun copies back <= 64 MiB): stats CSVs, our kernels' counter rows
+for d in pmc_fetch pmc_write pmc_tcc; do
+  f=$(find "$OUT/$d" -name "*counter_collection.csv" | head -1)
+  [ -n "$f" ] && { head -1 "$f"; grep -E "rbx::" "$f" | head -200; } > "$OUT/${d}_rbx_rows.csv"
+done
+find "$OUT" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/trace"
 echo "profile $TAG ok"
