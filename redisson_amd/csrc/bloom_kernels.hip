@@ -379,6 +379,107 @@ __global__ __launch_bounds__(256) void k_bloom_add_commit(KeysDev keys, uint64_t
     if (count) block_add_u64(added, count);
 }
 
+// ---- single-filter fast path: 8-byte entries (bit << 32 | key id), empty = ~0 ------------
+// The table is cleared (memset 0xff) before every chunk, so a claim is one CAS on an empty
+// slot; a slot already holding the same bit takes the 64-bit atomicMin (same high word, so
+// the minimum is the smallest key id); a lookup is one 8-byte load per probe.
+__device__ __forceinline__ void ht8_insert(unsigned long long *__restrict__ T, uint32_t log2cap, uint32_t idx,
+                                           uint32_t id) {
+    const uint64_t mask = (1ULL << log2cap) - 1;
+    const unsigned long long mine = ((unsigned long long)idx << 32) | id;
+    uint64_t slot = ht_slot(idx, log2cap);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long old = atomicCAS(&T[slot], ~0ULL, mine);
+        if (old == ~0ULL) return;
+        if ((uint32_t)(old >> 32) == idx) {
+            if ((uint32_t)old > id) atomicMin(&T[slot], mine);
+            return;
+        }
+        slot = (slot + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ uint32_t ht8_owner(const unsigned long long *__restrict__ T, uint32_t log2cap,
+                                              uint32_t idx) {
+    const uint64_t mask = (1ULL << log2cap) - 1;
+    uint64_t slot = ht_slot(idx, log2cap);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long e = T[slot];
+        if ((uint32_t)(e >> 32) == idx) return (uint32_t)e;
+        slot = (slot + 1) & mask;
+    }
+    return 0xffffffffu;
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_add_probe8(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                          FilterDesc f, unsigned long long *__restrict__ T,
+                                                          uint32_t log2cap, uint32_t *__restrict__ zmask) {
+    uint32_t maxidx = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, base + t, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        uint32_t zm = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+                zm |= 1u << j;
+                ht8_insert(T, log2cap, idxs[j], (uint32_t)t);
+            }
+        }
+        zmask[t] = zm;
+    }
+    // Redis string length: one atomic per wave (every SETBIT grows it to idx/8 + 1)
+    const uint64_t wmax = wave_max_u64(maxidx);
+    if ((threadIdx.x & 63) == 0 && nchunk) raise_redis_len(f.redis_len, (unsigned long long)(wmax >> 3) + 1ULL);
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_bloom_add_commit8(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                           FilterDesc f, const unsigned long long *__restrict__ T,
+                                                           uint32_t log2cap, const uint32_t *__restrict__ zmask,
+                                                           uint8_t *__restrict__ out_new,
+                                                           unsigned long long *__restrict__ count) {
+    uint64_t added = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint32_t zm = zmask[t];
+        bool isnew = false;
+        if (zm) {
+            uint64_t h1, h2;
+            hash_key<KLEN>(keys, base + t, h1, h2);
+            uint64_t h = h1;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((zm >> j) & 1u) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                    if (ht8_owner(T, log2cap, idx) == (uint32_t)t) {
+                        isnew = true;
+                        atomicOr(&f.bm[idx >> 5], bit_in_word(idx));
+                    }
+                }
+                h += (j & 1) ? h1 : h2;
+            }
+        }
+        if (out_new) out_new[base + t] = isnew;
+        added += isnew;
+    }
+    if (count) block_add_u64(added, count);
+}
+
 // Generic-k add (k > 32): per-pair zero flags in a byte array zflag[t*k + j].
 template <int KLEN>
 __global__ __launch_bounds__(256) void k_bloom_add_probe_anyk(KeysDev keys, uint64_t base, uint64_t nchunk,
@@ -548,6 +649,14 @@ void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const Filte
 template <int KLEN, int KMAX>
 static void launch_add_chunk_k(const AddChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(a.nchunk, kMaxGrid);
+    if (a.narrow) {
+        auto *T = (unsigned long long *)a.table;
+        hipLaunchKernelGGL((k_bloom_add_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                           a.single, T, a.log2cap, a.zmask);
+        hipLaunchKernelGGL((k_bloom_add_commit8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                           a.single, (const unsigned long long *)T, a.log2cap, a.zmask, a.out_new, a.count);
+        return;
+    }
     hipLaunchKernelGGL((k_bloom_add_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
                        a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch, a.zmask);
     hipLaunchKernelGGL((k_bloom_add_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,

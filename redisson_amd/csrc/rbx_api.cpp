@@ -492,6 +492,7 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
                    unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
     if (keys.n == 0) return RBX_OK;
     const uint64_t k = std::max<uint32_t>(kmax, 1);
+    const bool narrow = d_filt == nullptr && kmax <= 32;
     // chunk so that pairs per chunk <= 2^26 (table <= 2^27 entries at load <= 1/2)
     uint64_t chunk = std::min<uint64_t>(keys.n, (1ULL << 26) / k);
     chunk = std::max<uint64_t>(chunk, 1);
@@ -500,8 +501,19 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
-        RBX_TRY(ensure_table(c, nch * k, st));
         AddChunkArgs a{};
+        if (narrow) {
+            uint32_t lg = 16;
+            while (lg < 27 && (1ULL << lg) < 2 * nch * k) ++lg;
+            RBX_TRY(c->table.reserve(8ull << lg));
+            HIP_TRY(hipMemsetAsync(c->table.p, 0xff, 8ull << lg, st));
+            c->epoch = 255;  // the wide (16-byte) layout must be re-initialised before reuse
+            a.log2cap = lg;
+        } else {
+            RBX_TRY(ensure_table(c, nch * k, st));
+            a.log2cap = c->log2cap;
+            a.epoch = c->epoch;
+        }
         a.keys = keys;
         a.base = base;
         a.nchunk = nch;
@@ -510,13 +522,12 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
         a.nseg = nseg;
         a.single = single;
         a.table = c->table.as<HTEntry>();
-        a.log2cap = c->log2cap;
-        a.epoch = c->epoch;
         a.zmask = c->zmask.as<uint32_t>();
         a.kmax = kmax;
         a.out_new = d_out_new;
         a.count = d_count;
         a.seg_counts = d_seg_counts;
+        a.narrow = narrow;
         launch_bloom_add_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
     }

@@ -45,6 +45,7 @@ struct AddChunkArgs {
     uint8_t *out_new;
     unsigned long long *count;
     unsigned long long *seg_counts;
+    bool narrow;  // single filter, k <= 32: 8-byte entries, table cleared per chunk
 };
 
 // bloom_kernels.hip
