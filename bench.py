@@ -436,7 +436,7 @@ def main():
     log(f"[bench] rank {rank}/{world} workload {args.workload}")
     if args.workload == "c2":
         res = run_c2(args, world, rank, local)
-        if rank == 0 and not args.no_cpu_baseline:
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_c2(args.cpu_seconds)
     elif args.workload == "c4":
         res = run_c4(args, world, rank, local)

@@ -18,7 +18,9 @@
  *    several threads are safe.
  *  - *_dev variants take DEVICE pointers and a hipStream_t (as void*; NULL = the
  *    context's stream), enqueue work and return without synchronizing.  Counts are
- *    accumulated into device-resident unsigned long long words.
+ *    accumulated into device-resident unsigned long long words.  Per-call device scratch
+ *    of a context is stream-ordered: use one stream per context for *_dev calls (or
+ *    synchronize before switching streams).
  */
 #ifndef RBX_H
 #define RBX_H

@@ -201,18 +201,30 @@ __device__ __forceinline__ uint32_t upper_seg(const uint64_t *off, uint32_t nseg
     return lo;
 }
 
+// tile_seg0[t] = segment of key t*256 (one parallel binary search per 256-key tile)
+__global__ __launch_bounds__(256) void k_tile_seg0(const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                   uint64_t ntiles, uint32_t *__restrict__ tile_seg0) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) tile_seg0[t] = upper_seg(seg_off, nseg, t * 256);
+}
+
+// segment of key i, scanning forward from a lower bound s (off[s] <= i)
+__device__ __forceinline__ uint32_t seg_from(const uint64_t *__restrict__ off, uint32_t nseg, uint32_t s,
+                                             uint64_t i) {
+    while (s + 1 < nseg && off[s + 1] <= i) ++s;
+    return s;
+}
+
 template <int KLEN, int KMAX, int S1>
 __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, const FilterDesc *__restrict__ filt,
                                                               const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                              const uint32_t *__restrict__ tile_seg0,
                                                               uint8_t *__restrict__ out,
                                                               unsigned long long *__restrict__ counts) {
     __shared__ uint64_t s_off[257];
-    __shared__ uint32_t s_seg0;
     const uint64_t nkeys = keys.n;
     for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < nkeys; b0 += (uint64_t)gridDim.x * 256) {
-        if (threadIdx.x == 0) s_seg0 = upper_seg(seg_off, nseg, b0);
-        __syncthreads();
-        const uint32_t s0 = s_seg0;
+        const uint32_t s0 = tile_seg0[b0 >> 8];
         for (uint32_t t = threadIdx.x; t < 257; t += blockDim.x) {
             const uint32_t s = s0 + t;
             s_off[t] = s <= nseg ? seg_off[s] : ~0ULL;
@@ -297,6 +309,7 @@ template <int KLEN, int KMAX>
 __global__ __launch_bounds__(256) void k_bloom_add_probe(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                          const FilterDesc *__restrict__ filt,
                                                          const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                         const uint32_t *__restrict__ tile_seg0,
                                                          FilterDesc single, HTEntry *__restrict__ T,
                                                          uint32_t log2cap, uint32_t epoch,
                                                          uint32_t *__restrict__ zmask) {
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(256) void k_bloom_add_probe(KeysDev keys, uint64_t 
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
         const uint64_t i = base + t;
         FilterDesc f = single;
-        if (filt) f = filt[upper_seg(seg_off, nseg, i)];
+        if (filt) f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
         uint64_t h1, h2;
         hash_key<KLEN>(keys, i, h1, h2);
         uint32_t word[KMAX], idxs[KMAX];
@@ -338,6 +351,7 @@ template <int KLEN, int KMAX>
 __global__ __launch_bounds__(256) void k_bloom_add_commit(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                           const FilterDesc *__restrict__ filt,
                                                           const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                          const uint32_t *__restrict__ tile_seg0,
                                                           FilterDesc single, const HTEntry *__restrict__ T,
                                                           uint32_t log2cap, uint32_t epoch,
                                                           const uint32_t *__restrict__ zmask,
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(256) void k_bloom_add_commit(KeysDev keys, uint64_t
             uint32_t seg = 0;
             FilterDesc f = single;
             if (filt) {
-                seg = upper_seg(seg_off, nseg, i);
+                seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
                 f = filt[seg];
             }
             uint64_t h1, h2;
@@ -485,6 +499,7 @@ template <int KLEN>
 __global__ __launch_bounds__(256) void k_bloom_add_probe_anyk(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                               const FilterDesc *__restrict__ filt,
                                                               const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                              const uint32_t *__restrict__ tile_seg0,
                                                               FilterDesc single, HTEntry *__restrict__ T,
                                                               uint32_t log2cap, uint32_t epoch,
                                                               uint8_t *__restrict__ zflag, uint32_t kstride) {
@@ -492,7 +507,7 @@ __global__ __launch_bounds__(256) void k_bloom_add_probe_anyk(KeysDev keys, uint
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
         const uint64_t i = base + t;
         FilterDesc f = single;
-        if (filt) f = filt[upper_seg(seg_off, nseg, i)];
+        if (filt) f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
         uint64_t h1, h2;
         hash_key<KLEN>(keys, i, h1, h2);
         uint64_t h = h1;
@@ -513,6 +528,7 @@ template <int KLEN>
 __global__ __launch_bounds__(256) void k_bloom_add_commit_anyk(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                                const FilterDesc *__restrict__ filt,
                                                                const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                               const uint32_t *__restrict__ tile_seg0,
                                                                FilterDesc single, const HTEntry *__restrict__ T,
                                                                uint32_t log2cap, uint32_t epoch,
                                                                const uint8_t *__restrict__ zflag, uint32_t kstride,
@@ -526,7 +542,7 @@ __global__ __launch_bounds__(256) void k_bloom_add_commit_anyk(KeysDev keys, uin
         uint32_t seg = 0;
         FilterDesc f = single;
         if (filt) {
-            seg = upper_seg(seg_off, nseg, i);
+            seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
             f = filt[seg];
         }
         uint64_t h1, h2;
@@ -621,28 +637,36 @@ void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *b
 
 template <int KLEN>
 static void launch_contains_multi_k(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off,
-                                    uint32_t nseg, uint32_t kmax, uint8_t *out, unsigned long long *counts,
-                                    hipStream_t st, unsigned grid) {
+                                    uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax, uint8_t *out,
+                                    unsigned long long *counts, hipStream_t st, unsigned grid) {
     const bool dbl = g_stage1 == 4;
     if (kmax <= 8) {
-        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
-        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
+        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
     } else if (kmax <= 16) {
-        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
-        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+        if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
+        else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 16, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
     }
-    else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 0, 0>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, out, counts);
+    else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 0, 0>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
+}
+
+void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0,
+                      hipStream_t st) {
+    const uint64_t ntiles = (nkeys + 255) / 256;
+    if (!ntiles) return;
+    hipLaunchKernelGGL(k_tile_seg0, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, st, seg_off, nseg, ntiles,
+                       tile_seg0);
 }
 
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
-                                 const uint64_t *seg_off, uint32_t nseg, uint32_t kmax, uint8_t *out,
-                                 unsigned long long *counts, hipStream_t st) {
+                                 const uint64_t *seg_off, uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax,
+                                 uint8_t *out, unsigned long long *counts, hipStream_t st) {
     const unsigned grid = grid_for(keys.n, kMaxGrid);
     switch (klen_fast) {
-    case 16: launch_contains_multi_k<16>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
-    case 32: launch_contains_multi_k<32>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
-    case 64: launch_contains_multi_k<64>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
-    default: launch_contains_multi_k<0>(keys, filt, seg_off, nseg, kmax, out, counts, st, grid); break;
+    case 16: launch_contains_multi_k<16>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
+    case 32: launch_contains_multi_k<32>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
+    case 64: launch_contains_multi_k<64>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
+    default: launch_contains_multi_k<0>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
     }
 }
 
@@ -658,9 +682,9 @@ static void launch_add_chunk_k(const AddChunkArgs &a, hipStream_t st) {
         return;
     }
     hipLaunchKernelGGL((k_bloom_add_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
-                       a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch, a.zmask);
+                       a.filt, a.seg_off, a.nseg, a.tile_seg0, a.single, a.table, a.log2cap, a.epoch, a.zmask);
     hipLaunchKernelGGL((k_bloom_add_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
-                       a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch, a.zmask, a.out_new,
+                       a.filt, a.seg_off, a.nseg, a.tile_seg0, a.single, a.table, a.log2cap, a.epoch, a.zmask, a.out_new,
                        a.count, a.seg_counts);
 }
 
@@ -672,10 +696,10 @@ static void launch_add_chunk_len(const AddChunkArgs &a, hipStream_t st) {
     else {
         const unsigned grid = grid_for(a.nchunk, kMaxGrid);
         hipLaunchKernelGGL((k_bloom_add_probe_anyk<KLEN>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
-                           a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch,
+                           a.filt, a.seg_off, a.nseg, a.tile_seg0, a.single, a.table, a.log2cap, a.epoch,
                            (uint8_t *)a.zmask, a.kmax);
         hipLaunchKernelGGL((k_bloom_add_commit_anyk<KLEN>), dim3(grid), dim3(256), 0, st, a.keys, a.base,
-                           a.nchunk, a.filt, a.seg_off, a.nseg, a.single, a.table, a.log2cap, a.epoch,
+                           a.nchunk, a.filt, a.seg_off, a.nseg, a.tile_seg0, a.single, a.table, a.log2cap, a.epoch,
                            (const uint8_t *)a.zmask, a.kmax, a.out_new, a.count, a.seg_counts);
     }
 }

@@ -182,7 +182,9 @@ struct rbx_ctx {
     DevBuf zmask;
 
     // staging for host-buffer calls
-    DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc;
+    DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
+    std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
+    bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
     uint64_t filt_generation = 0;
     uint64_t generation = 1;  // bumped whenever a bitmap is (re)allocated or freed
@@ -520,6 +522,7 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
         a.filt = d_filt;
         a.seg_off = d_seg_off;
         a.nseg = nseg;
+        a.tile_seg0 = c->tile_segs.as<uint32_t>();
         a.single = single;
         a.table = c->table.as<HTEntry>();
         a.zmask = c->zmask.as<uint32_t>();
@@ -1048,8 +1051,8 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
                 memcmp(c->filt_cache.data(), v.data(), v.size() * sizeof(FilterDesc)) == 0;
     if (!same) {
         RBX_TRY(c->filt_table.reserve(v.size() * sizeof(FilterDesc)));
+        // pageable source: the runtime has staged it when the call returns
         HIP_TRY(hipMemcpyAsync(c->filt_table.p, v.data(), v.size() * sizeof(FilterDesc), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipStreamSynchronize(st));
         c->filt_cache.swap(v);
         c->filt_generation = c->generation;
     }
@@ -1068,8 +1071,10 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
-    launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, kmax, d_out,
-                                d_counts, st);
+    RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
+    launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+    launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg,
+                                c->tile_segs.as<uint32_t>(), kmax, d_out, d_counts, st);
     HIP_TRY(hipGetLastError());
     return RBX_OK;
 }
@@ -1086,6 +1091,8 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
+    RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
+    launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
     FilterDesc dummy{};
     return run_add(c, k, c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, dummy, kmax, d_out_new, nullptr,
                    d_counts, st);
@@ -1182,11 +1189,20 @@ static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64
                 tiles.push_back(HllSeg{hl[s]->d_regs, b, std::min(h_seg[s + 1], b + kTileElems), s, 0});
         }
         if (!tiles.empty()) {
-            RBX_TRY(c->ptrs.reserve(tiles.size() * sizeof(HllSeg)));
-            HIP_TRY(hipMemcpyAsync(c->ptrs.p, tiles.data(), tiles.size() * sizeof(HllSeg), hipMemcpyHostToDevice, st));
-            launch_hll_pfadd(dk, fl, c->ptrs.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
+            // the tile table is cached by content (a steady PFADD pipeline re-sends the same one)
+            const bool single_round = s0 == 0 && s1 == nseg;
+            const bool same = single_round && c->tiles_valid && c->tile_cache.size() == tiles.size() &&
+                              memcmp(c->tile_cache.data(), tiles.data(), tiles.size() * sizeof(HllSeg)) == 0;
+            if (!same) {
+                RBX_TRY(c->hll_tiles.reserve(tiles.size() * sizeof(HllSeg)));
+                // pageable source: staged by the runtime before the call returns; stream order
+                // keeps the previous round's kernel ahead of this overwrite
+                HIP_TRY(hipMemcpyAsync(c->hll_tiles.p, tiles.data(), tiles.size() * sizeof(HllSeg), hipMemcpyHostToDevice, st));
+                c->tiles_valid = single_round;
+                if (single_round) c->tile_cache = tiles;
+            }
+            launch_hll_pfadd(dk, fl, c->hll_tiles.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipStreamSynchronize(st));  // tiles vector reused next round
         }
         s0 = s1;
     }

@@ -37,6 +37,7 @@ struct AddChunkArgs {
     const FilterDesc *filt;  // nullable: single filter
     const uint64_t *seg_off;
     uint32_t nseg;
+    const uint32_t *tile_seg0;
     FilterDesc single;
     HTEntry *table;
     uint32_t log2cap, epoch;
@@ -51,9 +52,11 @@ struct AddChunkArgs {
 // bloom_kernels.hip
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
                            uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
+// tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)
+void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
-                                 const uint64_t *seg_off, uint32_t nseg, uint32_t kmax, uint8_t *out,
-                                 unsigned long long *counts, hipStream_t st);
+                                 const uint64_t *seg_off, uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax,
+                                 uint8_t *out, unsigned long long *counts, hipStream_t st);
 void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
 // random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe
