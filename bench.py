@@ -56,12 +56,20 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RBX_BENCH_SHARED_GPU=1 rehearses the multi-rank flow on a one-GPU box: every rank on
+    # cuda:0, gloo for the barrier / max-over-ranks (RCCL cannot put two ranks on one GPU).
+    shared = os.environ.get("RBX_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -383,7 +391,8 @@ def run_c4(args, world, rank, local):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.steps
     merge_ms = None
-    if world > 1:  # element-partitioned registers -> RCCL uint8 max all-reduce over xGMI
+    if world > 1 and os.environ.get("RBX_BENCH_SHARED_GPU") != "1":
+        # element-partitioned registers -> RCCL uint8 max all-reduce over xGMI
         import torch.distributed as dist
 
         uid = (C.c_uint8 * 128)()

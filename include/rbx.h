@@ -155,6 +155,17 @@ int rbx_bloom_add_multi(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
                         const uint64_t *seg_offsets, const rbx_keys *keys, uint8_t *out_new,
                         uint64_t *out_counts);
 
+/* Ordered mixed stream (BASELINE C5): key i is one contains(T) (key_op[i] = 0) or add(T)
+ * (key_op[i] = 1) on filters[key_filter[i]], executed in key order -- an add is visible to
+ * every later contains of the same filter, exactly as the commands would run one after
+ * another (M/RedissonBloomFilter.java:99-102, :198-201).  out (nullable): per key, present /
+ * newly added.  counts[0] = present contains, counts[1] = newly added.  k <= 32. */
+int rbx_bloom_stream_dev(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
+                         const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
+                         unsigned long long *d_counts, void *stream);
+int rbx_bloom_stream(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *key_filter,
+                     const uint8_t *key_op, const rbx_keys *keys, uint8_t *out, uint64_t *counts);
+
 /* ---- RHyperLogLog (by name) -- M/api/RHyperLogLog.java:27-68 -------------------- */
 /* add / addAll -> PFADD name e1..en   M/RedissonHyperLogLog.java:71-81.
  * *changed = 1 iff the key was created or any register changed. */

@@ -80,6 +80,8 @@ SIGNATURES = {
     "rbx_bloom_add_multi_dev": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, C.POINTER(RbxKeys), vp, vp, vp]),
     "rbx_bloom_contains_multi": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p, u64p]),
     "rbx_bloom_add_multi": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_stream_dev": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, vp, C.POINTER(RbxKeys), vp, vp, vp]),
+    "rbx_bloom_stream": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, u32p, u8p, C.POINTER(RbxKeys), u8p, u64p]),
     "rbx_hll_add": (C.c_int, [vp, C.c_char_p, C.POINTER(RbxKeys), C.POINTER(C.c_int)]),
     "rbx_hll_add_multi": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
     "rbx_hll_count": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p]),

@@ -277,6 +277,19 @@ def bloom_add_multi(client: RedissonClient, handles: list[BloomHandle], seg_offs
     return (counts, out[: arena.n]) if per_key else counts
 
 
+def bloom_stream(client: RedissonClient, handles: list[BloomHandle], key_filter, key_op, arena: Arena):
+    """Ordered mixed stream of single-key contains (op 0) / add (op 1) commands on
+    handles[key_filter[i]]; returns (per-key results, [present contains, newly added])."""
+    kf = np.ascontiguousarray(key_filter, dtype=np.uint32)
+    op = np.ascontiguousarray(key_op, dtype=np.uint8)
+    out = np.zeros(max(arena.n, 1), np.uint8)
+    counts = np.zeros(2, np.uint64)
+    _check(L.lib().rbx_bloom_stream(client.ctx, _handles(handles), len(handles), kf.ctypes.data_as(L.u32p),
+                                    op.ctypes.data_as(L.u8p), arena.ptr(), out.ctypes.data_as(L.u8p),
+                                    counts.ctypes.data_as(L.u64p)))
+    return out[: arena.n], counts
+
+
 class RHyperLogLog:
     """M/RedissonHyperLogLog.java (PFADD / PFCOUNT / PFMERGE)."""
 

@@ -393,6 +393,152 @@ __global__ __launch_bounds__(256) void k_bloom_add_commit(KeysDev keys, uint64_t
     if (count) block_add_u64(added, count);
 }
 
+// Looks keypart up; ~0u when absent (linear probing never leaves an unclaimed slot before an
+// entry, so the first slot not claimed in this epoch ends the search).
+__device__ __forceinline__ uint32_t ht_find(const HTEntry *__restrict__ T, uint32_t log2cap, uint32_t epoch,
+                                            uint64_t keypart) {
+    const uint64_t mask = (1ULL << log2cap) - 1;
+    const uint64_t mytag = ((uint64_t)epoch << 56) | keypart;
+    uint64_t slot = ht_slot(keypart, log2cap);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const HTEntry e = T[slot];
+        if (e.tag == mytag) return (uint32_t)e.idw;
+        if ((uint32_t)(e.tag >> 56) != epoch) return 0xffffffffu;
+        slot = (slot + 1) & mask;
+    }
+    return 0xffffffffu;
+}
+
+// ---- ordered mixed stream (C5): key i is a single-key contains (op 0) or add (op 1) on
+// filters[kf[i]], executed in key order.  Per chunk: probe the adds (first-setter table of
+// add positions per initially-zero bit), then the contains -- a zero bit counts as set iff an
+// add at an earlier position of the chunk touches it -- then commit the adds.  Earlier chunks
+// are committed before later ones probe, so chunking keeps the order.
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                      const FilterDesc *__restrict__ filt,
+                                                      const uint32_t *__restrict__ kf, const uint8_t *__restrict__ op,
+                                                      HTEntry *__restrict__ T, uint32_t log2cap, uint32_t epoch,
+                                                      uint32_t *__restrict__ zmask) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        uint32_t zm = 0;
+        if (op[i]) {
+            const FilterDesc f = filt[kf[i]];
+            uint64_t h1, h2;
+            hash_key<KLEN>(keys, i, h1, h2);
+            uint32_t word[KMAX], idxs[KMAX];
+            uint32_t maxidx = 0;
+            uint64_t h = h1;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((uint32_t)j < f.k) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                    idxs[j] = idx;
+                    word[j] = f.bm[idx >> 5];
+                    maxidx = idx > maxidx ? idx : maxidx;
+                }
+                h += (j & 1) ? h1 : h2;
+            }
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+                    zm |= 1u << j;
+                    ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], (uint32_t)t);
+                }
+            }
+            raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+        }
+        zmask[t] = zm;
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                         const FilterDesc *__restrict__ filt,
+                                                         const uint32_t *__restrict__ kf,
+                                                         const uint8_t *__restrict__ op,
+                                                         const HTEntry *__restrict__ T, uint32_t log2cap,
+                                                         uint32_t epoch, uint8_t *__restrict__ out,
+                                                         unsigned long long *__restrict__ counts) {
+    uint64_t present = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        if (op[i]) continue;
+        const FilterDesc f = filt[kf[i]];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        // doubling stages 1, 2, 4, ...: all loads of a stage in flight, stop at a clear bit
+        bool all = true;
+        uint64_t h = h1;
+        uint32_t j = 0;
+        for (uint32_t width = 1; j < f.k && all; width <<= 1) {
+            uint32_t word[KMAX], idxs[KMAX];
+            const uint32_t e = min(f.k, j + width);
+#pragma unroll
+            for (int u = 0; u < KMAX; ++u) {
+                if (j + u < e) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                    idxs[u] = idx;
+                    word[u] = f.bm[idx >> 5];
+                    h += ((j + u) & 1) ? h1 : h2;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < KMAX; ++u) {
+                if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
+                    const uint32_t owner = ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
+                    all = owner < (uint32_t)t;  // set by an earlier add of this chunk
+                }
+            }
+            j = e;
+        }
+        if (out) out[i] = all;
+        present += all;
+    }
+    if (counts) block_add_u64(present, counts);
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                       const FilterDesc *__restrict__ filt,
+                                                       const uint32_t *__restrict__ kf,
+                                                       const uint8_t *__restrict__ op, const HTEntry *__restrict__ T,
+                                                       uint32_t log2cap, uint32_t epoch,
+                                                       const uint32_t *__restrict__ zmask, uint8_t *__restrict__ out,
+                                                       unsigned long long *__restrict__ counts) {
+    uint64_t added = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        if (!op[i]) continue;
+        const uint32_t zm = zmask[t];
+        bool isnew = false;
+        if (zm) {
+            const FilterDesc f = filt[kf[i]];
+            uint64_t h1, h2;
+            hash_key<KLEN>(keys, i, h1, h2);
+            uint64_t h = h1;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((zm >> j) & 1u) {
+                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                    if (ht_owner(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx) == (uint32_t)t) {
+                        isnew = true;
+                        atomicOr(&f.bm[idx >> 5], bit_in_word(idx));
+                    }
+                }
+                h += (j & 1) ? h1 : h2;
+            }
+        }
+        if (out) out[i] = isnew;
+        added += isnew;
+    }
+    if (counts) block_add_u64(added, counts + 1);
+}
+
 // ---- single-filter fast path: 8-byte entries (bit << 32 | key id), empty = ~0 ------------
 // The table is cleared (memset 0xff) before every chunk, so a claim is one CAS on an empty
 // slot; a slot already holding the same bit takes the 64-bit atomicMin (same high word, so
@@ -710,6 +856,33 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
     case 32: launch_add_chunk_len<32>(a, st); break;
     case 64: launch_add_chunk_len<64>(a, st); break;
     default: launch_add_chunk_len<0>(a, st); break;
+    }
+}
+
+template <int KLEN, int KMAX>
+static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
+    const unsigned grid = grid_for(a.nchunk, kMaxGrid);
+    hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.zmask);
+    hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.out, a.counts);
+    hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
+}
+
+template <int KLEN>
+static void launch_stream_chunk_len(const StreamChunkArgs &a, hipStream_t st) {
+    if (a.kmax <= 8) launch_stream_chunk_k<KLEN, 8>(a, st);
+    else if (a.kmax <= 16) launch_stream_chunk_k<KLEN, 16>(a, st);
+    else launch_stream_chunk_k<KLEN, 32>(a, st);
+}
+
+void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st) {
+    switch (klen_fast) {
+    case 16: launch_stream_chunk_len<16>(a, st); break;
+    case 32: launch_stream_chunk_len<32>(a, st); break;
+    case 64: launch_stream_chunk_len<64>(a, st); break;
+    default: launch_stream_chunk_len<0>(a, st); break;
     }
 }
 

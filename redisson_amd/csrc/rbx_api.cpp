@@ -1098,6 +1098,87 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
                    d_counts, st);
 }
 
+// Ordered mixed stream (C5): see rbx.h.  Chunks of <= 2^26 pairs run probe -> contains -> commit.
+int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
+                         const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
+                         unsigned long long *d_counts, void *stream) {
+    if (!c || !filters || nfilters == 0 || !d_key_filter || !d_key_op)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    RBX_TRY(validate_keys(d_keys));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    hipStream_t st = pick_stream(c, stream);
+    uint32_t kmax;
+    RBX_TRY(upload_filters(c, filters, nfilters, &kmax, st));
+    if (kmax > 32) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream batches support k <= 32");
+    if (d_keys->n == 0) return RBX_OK;
+    KeysDev keys = keys_dev(d_keys);
+    const uint64_t k = std::max<uint32_t>(kmax, 1);
+    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, (1ULL << 26) / k));
+    RBX_TRY(c->zmask.reserve(chunk * 4));
+    const int fl = fast_len(keys);
+    for (uint64_t base = 0; base < keys.n; base += chunk) {
+        const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
+        RBX_TRY(ensure_table(c, nch * k, st));
+        StreamChunkArgs s{};
+        s.keys = keys;
+        s.base = base;
+        s.nchunk = nch;
+        s.filt = c->filt_table.as<FilterDesc>();
+        s.kf = d_key_filter;
+        s.op = d_key_op;
+        s.table = c->table.as<HTEntry>();
+        s.log2cap = c->log2cap;
+        s.epoch = c->epoch;
+        s.zmask = c->zmask.as<uint32_t>();
+        s.kmax = kmax;
+        s.out = d_out;
+        s.counts = d_counts;
+        launch_stream_chunk(s, fl, st);
+        HIP_TRY(hipGetLastError());
+    }
+    return RBX_OK;
+}
+
+int rbx_bloom_stream(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *key_filter,
+                     const uint8_t *key_op, const rbx_keys *keys, uint8_t *out, uint64_t *counts) {
+    if (!c || !filters || nfilters == 0 || !key_filter || !key_op) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    RBX_TRY(validate_keys(keys));
+    for (uint64_t i = 0; i < keys->n; ++i)
+        if (key_filter[i] >= nfilters) return fail(RBX_E_ILLEGAL_ARGUMENT, "key_filter index out of range");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RBX_TRY(set_device(c));
+    KeysDev dk;
+    RBX_TRY(upload_keys(c, keys, 0, keys->n, &dk));
+    const uint64_t n = keys->n;
+    RBX_TRY(c->seg_offs.reserve(n * 4 + n + 64));
+    auto *d_kf = c->seg_offs.as<uint32_t>();
+    auto *d_op = (uint8_t *)(d_kf + n);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(d_kf, key_filter, n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_op, key_op, n, hipMemcpyHostToDevice, c->stream));
+    }
+    RBX_TRY(c->counters.reserve(64));
+    auto *d_cnt = c->counters.as<unsigned long long>() + 2;
+    HIP_TRY(hipMemsetAsync(d_cnt, 0, 16, c->stream));
+    uint8_t *d_out = nullptr;
+    if (out) {
+        RBX_TRY(c->out_bytes.reserve(n));
+        d_out = c->out_bytes.as<uint8_t>();
+    }
+    rbx_keys kd{dk.bytes, dk.offsets, dk.stride, dk.n};
+    RBX_TRY(rbx_bloom_stream_dev(c, filters, nfilters, d_kf, d_op, &kd, d_out, d_cnt, c->stream));
+    if (out && n) HIP_TRY(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long cnt[2];
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (counts) {
+        counts[0] = cnt[0];
+        counts[1] = cnt[1];
+    }
+    return RBX_OK;
+}
+
 static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *seg_offsets,
                       const rbx_keys *keys, uint8_t *out_flags, uint64_t *out_counts, bool is_add) {
     if (!c || !filters || !seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");

@@ -49,7 +49,23 @@ struct AddChunkArgs {
     bool narrow;  // single filter, k <= 32: 8-byte entries, table cleared per chunk
 };
 
+// ordered mixed contains/add stream (one chunk of keys)
+struct StreamChunkArgs {
+    KeysDev keys;
+    uint64_t base, nchunk;
+    const FilterDesc *filt;
+    const uint32_t *kf;   // per key: index into filt
+    const uint8_t *op;    // per key: 0 contains, 1 add
+    HTEntry *table;
+    uint32_t log2cap, epoch;
+    uint32_t *zmask;
+    uint32_t kmax;
+    uint8_t *out;         // per key: present (contains) / newly added (add)
+    unsigned long long *counts;  // [0] present contains, [1] new adds
+};
+
 // bloom_kernels.hip
+void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
                            uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
 // tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)

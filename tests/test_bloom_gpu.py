@@ -446,3 +446,46 @@ def test_contains_schedules_identical(client, fresh, sched):
         cr, pr = ref.contains(*O.fixed_arena(mat), per_key=True)
         assert cg == cr and np.array_equal(pg, pr)
         f.delete()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_mixed_stream_in_order_semantics(client, fresh, seed):
+    """C5 shape: an ordered stream of single-key contains/add commands over tenants with a
+    skewed tenant choice; every answer equals the one-after-another oracle replay, including
+    contains right after an add of the same key and adds racing on shared bits."""
+    from redisson_amd import bloom_stream
+
+    rng = np.random.default_rng(seed)
+    shapes = [(64, 7), (729, 5), (9585, 7), (14377587, 10), (100003, 17)]
+    names = [f"{fresh}-{i}" for i in range(len(shapes))]
+    refs = []
+    for n, (m, k) in zip(names, shapes):
+        client.getBloomFilter(n).tryInitRaw(m, k)
+        refs.append(O.OracleBloom(m, k))
+    handles = [BloomHandle(client, n) for n in names]
+    handles.append(handles[1])  # the same filter under a second index
+    alias = {len(shapes): 1}
+    nkeys = 6000
+    pool = [rng.bytes(int(L)) for L in rng.integers(0, 40, size=800)]
+    kf = np.minimum(rng.zipf(1.3, size=nkeys) - 1, len(handles) - 1).astype(np.uint32)
+    op = (rng.random(nkeys) < 0.3).astype(np.uint8)
+    keys = [pool[int(j)] for j in rng.integers(0, len(pool), size=nkeys)]
+    for i in range(0, nkeys, 97):  # contains of a key right after its add
+        if i + 1 < nkeys:
+            op[i], op[i + 1] = 1, 0
+            kf[i + 1] = kf[i]
+            keys[i + 1] = keys[i]
+    out, counts = bloom_stream(client, handles, kf, op, Arena(keys))
+    want = np.zeros(nkeys, np.uint8)
+    for i in range(nkeys):
+        r = refs[alias.get(int(kf[i]), int(kf[i]))]
+        b, o = O.arena([keys[i]])
+        want[i] = r.add(b, o) if op[i] else r.contains(b, o)
+    assert np.array_equal(out, want)
+    assert counts[0] == int(want[op == 0].sum()) and counts[1] == int(want[op == 1].sum())
+    for n, r in zip(names, refs):
+        assert client.getBloomFilter(n).exportBitmap() == r.redis_string()
+    for h in handles[:-1]:
+        h.close()
+    for n in names:
+        client.getBloomFilter(n).delete()
