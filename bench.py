@@ -38,11 +38,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     p.add_argument("--keys", type=int, default=100_000_000, help="keys (C2/C3) or elements (C4) per step per GPU")
     p.add_argument("--tenants", type=int, default=100_000, help="C3 tenant count (whole node)")
     p.add_argument("--elements", type=int, default=1_000_000_000, help="C4 PFADD elements per step per GPU")
     p.add_argument("--stage1", type=int, default=None, help="contains early-exit schedule (rbx_tune)")
+    p.add_argument("--zipf-s", type=float, default=1.0, help="C5 tenant skew")
+    p.add_argument("--add-fraction", type=float, default=0.1, help="C5 share of add commands")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -347,6 +349,89 @@ def run_c3(args, world, rank, local):
 
 
 # ------------------------------------------------------------------------------------------
+# C5: ordered 90/10 contains/add stream, Zipf(1.0) tenants over the C3 set, 64-byte keys
+# ------------------------------------------------------------------------------------------
+def run_c5(args, world, rank, local):
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from redisson_amd import BloomHandle, RedissonClient, calc_slot, device_keys, slot_to_gpu
+    from redisson_amd import _lib as L
+
+    NT = args.tenants
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+    client = RedissonClient(local)
+    names = [f"tenant:{t:06d}" for t in range(NT)]
+    ranks = np.arange(1, NT + 1, dtype=np.float64)  # Zipf popularity rank of tenant t is t+1
+    mine = [t for t in range(NT) if slot_to_gpu(calc_slot(names[t]), world) == rank]
+    nt = len(mine)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0005 + rank)
+    pool = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+    rng = np.random.default_rng(rank)
+    handles = []
+    for t in mine:
+        f = client.getBloomFilter(names[t])
+        f.tryInit(1_000_000, 1e-3)
+        nbytes = (f._size + 7) // 8
+        off = int(rng.integers(0, (pool.numel() - nbytes) // 256)) * 256
+        assert L.lib().rbx_bloom_import_dev(client.ctx, names[t].encode(), pool.data_ptr() + off, nbytes, sptr) == 0
+        handles.append(BloomHandle(client, names[t]))
+    n = args.keys
+    w = torch.tensor(1.0 / ranks[mine] ** args.zipf_s, dtype=torch.float64, device="cuda")
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(n, dtype=torch.float64, device="cuda", generator=g)
+    kf = torch.searchsorted(cdf, u).clamp_(max=nt - 1).to(torch.int32)
+    op = (torch.rand(n, device="cuda", generator=g) < args.add_fraction).to(torch.uint8)
+    keys = torch.randint(0, 256, (n, 64), dtype=torch.uint8, device="cuda", generator=g)
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    arr = (C.c_void_p * nt)(*[h.h.value for h in handles])
+    dk = device_keys(keys.data_ptr(), n, 64)
+
+    def step():
+        assert L.lib().rbx_bloom_stream_dev(client.ctx, arr, nt, kf.data_ptr(), op.data_ptr(), C.byref(dk), None,
+                                             counts.data_ptr(), sptr) == 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    step_s = max_over_ranks(world, ms / 1e3)
+    value = sum_over_ranks(world, n) / step_s
+    top = int(torch.bincount(kf.long(), minlength=nt).max().item())
+    res = {
+        "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
+        "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"C5 ordered stream of {n} single-key commands ({args.add_fraction:.0%} add) over "
+                               f"{nt} tenant filters tryInit(1e6,1e-3) at design fill, Zipf(s={args.zipf_s}) tenants, "
+                               "64-byte keys, in-order semantics",
+                   "tenants_this_gpu": nt, "ops_per_gpu": n, "hottest_tenant_ops": top,
+                   "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": n * (64 + 10 * 8) / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": n * (64 + 10 * 8) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms},
+    }
+    for h in handles:
+        h.close()
+    client.shutdown()
+    return res
+
+
+# ------------------------------------------------------------------------------------------
 # C4: 10k HLLs, PFADD of 16-byte elements, PFCOUNT of all, RCCL max merge
 # ------------------------------------------------------------------------------------------
 def run_c4(args, world, rank, local):
@@ -449,6 +534,8 @@ def main():
             res["cpu_baseline"] = cpu_baseline_c2(args.cpu_seconds)
     elif args.workload == "c4":
         res = run_c4(args, world, rank, local)
+    elif args.workload == "c5":
+        res = run_c5(args, world, rank, local)
     else:
         res = run_c3(args, world, rank, local)
     if rank == 0:
