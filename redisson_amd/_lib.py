@@ -101,6 +101,7 @@ SIGNATURES = {
     "rbx_hll_allreduce_max": (C.c_int, [vp, C.POINTER(vp), C.c_uint32]),
     "rbx_bench_gather": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, vp]),
     "rbx_tune": (C.c_int, [C.c_char_p, C.c_int]),
+    "rbx_bench_gather_regions": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint, vp, vp]),
     # include/rbx_selftest.h
     "rbx_selftest_mod": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "rbx_selftest_hash128": (None, [u8p, C.c_uint64, u64p]),

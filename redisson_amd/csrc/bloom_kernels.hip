@@ -931,3 +931,42 @@ void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, u
     }
 }
 }  // namespace rbx
+
+// ---------------------------------------------------------------------------------
+// Region-local gather probe: the table is cut into regions of `region_words`; workgroup b
+// works on regions b%8, b%8+8, ... in order (blocks b and b+8 share an XCD under the
+// observed round-robin placement -- speed only), each lane doing k random loads inside the
+// current region.  Measures the L2-resident gather rate a region-bucketed probe can reach.
+// ---------------------------------------------------------------------------------
+namespace rbx {
+__global__ __launch_bounds__(256) void k_gather_regions(const uint32_t *__restrict__ tbl, uint64_t nregions,
+                                                        uint64_t region_words, uint64_t per_region,
+                                                        uint32_t *__restrict__ sink) {
+    const uint32_t xcd = blockIdx.x & 7, local = blockIdx.x >> 3, nlocal = gridDim.x >> 3;
+    uint32_t acc = 0;
+    for (uint64_t r = xcd; r < nregions; r += 8) {
+        const uint32_t *base = tbl + r * region_words;
+        for (uint64_t i = (uint64_t)local * blockDim.x + threadIdx.x; i < per_region; i += (uint64_t)nlocal * blockDim.x) {
+            uint64_t z = (r * 0x9E3779B97F4A7C15ULL) ^ (i * 0xBF58476D1CE4E5B9ULL);
+            z ^= z >> 31;
+            z *= 0x94D049BB133111EBULL;
+            uint32_t w[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                w[j] = base[(uint64_t)(uint32_t)(z >> (j & 1 ? 32 : 0) ^ (j * 0x9E3779B9u)) * region_words >> 32];
+                z += 0x632BE59BD9B4E019ULL;
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) acc ^= w[j];
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
+                           uint32_t *sink, hipStream_t st, unsigned grid) {
+    const uint64_t nregions = nwords / region_words;
+    hipLaunchKernelGGL(k_gather_regions, dim3(grid), dim3(256), 0, st, tbl, nregions, region_words,
+                       total_lanes / nregions, sink);
+}
+}  // namespace rbx

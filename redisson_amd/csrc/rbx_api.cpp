@@ -183,6 +183,7 @@ struct rbx_ctx {
 
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
+    DevBuf pc_surv_h, pc_surv_key, pc_surv_cnt, pc_bits, pc_hist, pc_scan, pc_pairs;  // partitioned contains
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
@@ -537,6 +538,73 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
     return RBX_OK;
 }
 
+// Partitioned contains (contains_partitioned.hip) for one large filter.  Mode: 0 never,
+// 1 whenever k in [2, 16], 2 when the bitmap exceeds 16 MiB and the batch >= 1M keys.  Default 0:
+// on MI355X the direct early-exit kernel is faster (DESIGN.md §3.6 has the measurements).
+static int g_partition_mode = 0;
+
+static bool use_partitioned(uint64_t size, uint32_t k, uint64_t n) {
+    if (k < 2 || k > 16 || size > (1ULL << 32)) return false;
+    if (g_partition_mode == 0) return false;
+    if (g_partition_mode == 1) return true;
+    return size > (128ULL << 20) && n >= (1ULL << 20);
+}
+
+static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,
+                                    unsigned long long *d_count, hipStream_t st) {
+    const uint32_t k = f.k;
+    const uint32_t nregions = (uint32_t)((f.mp.size + (1ULL << kPcRegionBits) - 1) >> kPcRegionBits);
+    uint64_t chunk = std::min<uint64_t>(1ULL << 27, (1ULL << 30) / (k - 1));
+    const uint64_t nch = (keys.n + chunk - 1) / chunk;
+    chunk = (keys.n + nch - 1) / nch;
+    chunk = (chunk + kPcTileKeys - 1) / kPcTileKeys * kPcTileKeys;
+    const uint64_t ntiles = chunk / kPcTileKeys;
+    const uint64_t ngroups = (chunk + 63) / 64;
+    RBX_TRY(c->pc_surv_h.reserve(chunk * 16));
+    RBX_TRY(c->pc_surv_key.reserve(chunk * 4));
+    RBX_TRY(c->pc_surv_cnt.reserve(ntiles * 4));
+    RBX_TRY(c->pc_bits.reserve(ngroups * 16));
+    RBX_TRY(c->pc_hist.reserve((uint64_t)nregions * ntiles * 4));
+    RBX_TRY(c->pc_scan.reserve((2 * (uint64_t)nregions + 1) * 8));
+    RBX_TRY(c->pc_pairs.reserve(chunk * (k - 1) * 8));
+    const int fl = fast_len(keys);
+    for (uint64_t base = 0; base < keys.n; base += chunk) {
+        PcArgs a{};
+        a.keys = keys;
+        a.base = base;
+        a.nchunk = std::min<uint64_t>(chunk, keys.n - base);
+        a.bm = f.bm;
+        a.mp = f.mp;
+        a.k = k;
+        a.nregions = nregions;
+        a.surv_h = c->pc_surv_h.as<uint4>();
+        a.surv_key = c->pc_surv_key.as<uint32_t>();
+        a.surv_cnt = c->pc_surv_cnt.as<uint32_t>();
+        a.survive_bits = c->pc_bits.as<unsigned long long>();
+        a.miss = a.survive_bits + ngroups;
+        a.hist = c->pc_hist.as<uint32_t>();
+        a.totals = c->pc_scan.as<unsigned long long>();
+        a.rbase = a.totals + nregions;
+        a.pairs = c->pc_pairs.as<unsigned long long>();
+        a.probe_grid = 2048;
+        a.out = d_out;
+        a.count = d_count;
+        HIP_TRY(hipMemsetAsync(a.miss, 0, ngroups * 8, st));
+        launch_contains_partitioned_chunk(a, fl, st);
+        HIP_TRY(hipGetLastError());
+    }
+    return RBX_OK;
+}
+
+// contains over device keys for one filter: direct (staged early exit) or partitioned
+static int run_contains(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,
+                        unsigned long long *d_count, hipStream_t st) {
+    if (use_partitioned(f.mp.size, f.k, keys.n)) return run_contains_partitioned(c, keys, f, d_out, d_count, st);
+    launch_bloom_contains(keys, fast_len(keys), f.bm, f.mp, f.k, d_out, d_count, st);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
 static FilterDesc desc_of(const Bitmap &b, uint64_t size, uint32_t k, uint32_t fid) {
     FilterDesc f{};
     f.bm = b.d_words;
@@ -781,8 +849,7 @@ static int bloom_host_op(rbx_ctx *c, const char *name, uint64_t size, uint32_t k
         if (is_add) {
             RBX_TRY(run_add(c, dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream));
         } else {
-            launch_bloom_contains(dk, fast_len(dk), f.bm, f.mp, k, d_out, d_count, c->stream);
-            HIP_TRY(hipGetLastError());
+            RBX_TRY(run_contains(c, dk, f, d_out, d_count, c->stream));
         }
         if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags + i0, d_out, n, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1014,9 +1081,7 @@ int rbx_bloom_contains_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uin
     RBX_TRY(set_device(c));
     KeysDev k = keys_dev(d_keys);
     FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
-    launch_bloom_contains(k, fast_len(k), f.bm, f.mp, b->k, d_out, d_count, pick_stream(c, stream));
-    HIP_TRY(hipGetLastError());
-    return RBX_OK;
+    return run_contains(c, k, f, d_out, d_count, pick_stream(c, stream));
 }
 
 int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out_new,
@@ -1782,9 +1847,25 @@ int rbx_bench_gather(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint
     return RBX_OK;
 }
 
+int rbx_bench_gather_regions(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint64_t region_bytes,
+                             uint64_t nlanes, unsigned grid, void *d_sink, void *stream) {
+    if (!c || !d_table || !d_sink || region_bytes < 4 || table_bytes < region_bytes || grid < 8)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    RBX_TRY(set_device(c));
+    launch_gather_regions((const uint32_t *)d_table, table_bytes / 4, region_bytes / 4, nlanes, (uint32_t *)d_sink,
+                          pick_stream(c, stream), grid & ~7u);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
 // Tuning knobs (process-wide).  "contains_stage1": early-exit width of contains (0 = off).
 int rbx_tune(const char *key, int value) {
     if (!key) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key");
+    if (!strcmp(key, "contains_partition")) {
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition in [0, 2]");
+        g_partition_mode = value;
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_stage1")) {
         if (value < 0 || value > 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1 in [0, 4]");
         set_contains_stage1(value);

@@ -49,6 +49,35 @@ struct AddChunkArgs {
     bool narrow;  // single filter, k <= 32: 8-byte entries, table cleared per chunk
 };
 
+// partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
+struct PcArgs {
+    KeysDev keys;
+    uint64_t base, nchunk;
+    const uint32_t *bm;
+    ModParams mp;
+    uint32_t k;
+    uint32_t nregions;      // ceil(size / 2^23)
+    uint4 *surv_h;          // nchunk records
+    uint32_t *surv_key;     // nchunk
+    uint32_t *surv_cnt;     // per tile
+    unsigned long long *survive_bits;  // ceil(nchunk/64)
+    unsigned long long *miss;          // ceil(nchunk/64), zeroed
+    uint32_t *hist;         // nregions x ntiles
+    unsigned long long *totals;        // nregions
+    unsigned long long *rbase;         // nregions + 1
+    unsigned long long *pairs;         // <= (k-1) * nchunk
+    unsigned probe_grid;
+    uint8_t *out;
+    unsigned long long *count;
+};
+constexpr uint64_t kPcTileKeys = 8192;
+constexpr uint32_t kPcRegionBits = 23;
+inline unsigned grid_for_pc(uint64_t n) {
+    uint64_t g = ((n + 63) / 64 + 255) / 256;
+    return (unsigned)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
+
 // ordered mixed contains/add stream (one chunk of keys)
 struct StreamChunkArgs {
     KeysDev keys;
@@ -75,6 +104,9 @@ void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const Filte
                                  uint8_t *out, unsigned long long *counts, hipStream_t st);
 void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
+// region-local gathers: 6 loads per lane inside XCD-assigned regions (partitioned-probe roofline)
+void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
+                           uint32_t *sink, hipStream_t st, unsigned grid);
 // random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe
 void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
                          hipStream_t st);

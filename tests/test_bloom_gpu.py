@@ -489,3 +489,38 @@ def test_mixed_stream_in_order_semantics(client, fresh, seed):
         h.close()
     for n in names:
         client.getBloomFilter(n).delete()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
+                                      (14377587, 2, 64), (95850583, 16, 0), (8388608 * 3 + 5, 5, 24)])
+def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
+    """The region-bucketed contains (forced on, mode 1) and the direct kernel (mode 0) give the
+    oracle's per-key answers; sizes that are not a multiple of the 1 MiB region included."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(size % 1000 + k * 7 + L)
+    n = 300_000
+    if L:
+        mat = rng.integers(0, 256, size=(n, L), dtype=np.uint8)
+        a_add, a_probe = Arena.fixed(mat[: n // 2]), Arena.fixed(mat)
+        o_add, o_probe = O.fixed_arena(mat[: n // 2]), O.fixed_arena(mat)
+    else:
+        keys = [rng.bytes(int(x)) for x in rng.integers(0, 90, size=n)]
+        a_add, a_probe = Arena(keys[: n // 2]), Arena(keys)
+        o_add, o_probe = O.arena(keys[: n // 2]), O.arena(keys)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(size, k)
+    ref = O.OracleBloom(size, k)
+    f.add(a_add)
+    ref.add(*o_add)
+    assert L_.lib().rbx_tune(b"contains_partition", mode) == 0
+    try:
+        cg, pg = f.containsEach(a_probe)
+        c2 = f.contains(a_probe)
+    finally:
+        L_.lib().rbx_tune(b"contains_partition", 0)
+    cr, pr = ref.contains(*o_probe, per_key=True)
+    assert cg == cr == c2
+    assert np.array_equal(pg, pr)
+    f.delete()

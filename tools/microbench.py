@@ -60,6 +60,48 @@ def main():
                   flush=True)
             del tb
 
+    if "regions" in a.what:
+        tb = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+        tb.random_(0, 255, generator=g)
+        lanes = 54_000_000  # survivors of stage 1 at C2, 6 remaining loads each
+        for rmb in [1, 2, 4, 8]:
+            for grid in [2048, 4096, 8192]:
+                f = lambda: L.lib().rbx_bench_gather_regions(client.ctx, tb.data_ptr(), tb.numel(), rmb << 20, lanes,
+                                                             grid, sink.data_ptr(), sp)
+                f()
+                ms = timed(stream, f, 3)
+                print(json.dumps({"bench": "gather_regions", "region_MiB": rmb, "grid": grid, "ms": ms,
+                                  "gathers_per_s": lanes * 6 / (ms / 1e3)}), flush=True)
+        del tb
+
+    if "partition" in a.what:
+        cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+        for name, size, k, n_add in [("C2_2^32", 1 << 32, 7, n // 2), ("C2_twin", 4294967293, 7, n // 2),
+                                     ("C1", 95850583, 7, 10_000_000)]:
+            fb = client.getBloomFilter("pc-" + name)
+            fb.tryInitRaw(size, k)
+            h = BloomHandle(client, "pc-" + name)
+            h.add_dev(device_keys(keys.data_ptr(), n_add, 32), cnt.data_ptr(), stream=sp)
+            torch.cuda.synchronize()
+            dk = device_keys(keys.data_ptr(), n, 32)
+            res = {0: [], 1: []}
+            counts = {}
+            for rnd in range(5):
+                for mode in res:
+                    L.lib().rbx_tune(b"contains_partition", mode)
+                    cnt[1].zero_()
+                    res[mode].append(timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 8, stream=sp), 2))
+                    counts[mode] = int(cnt[1].item())
+            assert counts[0] == counts[1], counts
+            for mode, v in res.items():
+                med = statistics.median(v)
+                print(json.dumps({"bench": "contains_partition", "filter": name, "mode": mode, "ms_median": med,
+                                  "ms_min": min(v), "keys_per_s": n / (med / 1e3), "present_x2": counts[mode]}),
+                      flush=True)
+            L.lib().rbx_tune(b"contains_partition", 0)
+            h.close()
+            fb.delete()
+
     if "stage1" in a.what or "sizes" in a.what:
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
         plan = []
