@@ -104,17 +104,42 @@ RBX_HD void hh_reset(HH &s) {
 // Each half is 1-2 v_perm_b32 byte shuffles after selection by the compiler.
 RBX_HD uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xffu; }
 
+// v_perm_b32: byte i of the result = byte sel[i] of the 8-byte value {hi:x, lo:y}
+// (selectors 0-3 pick y, 4-7 pick x, 0x0c gives 0).  The host build emulates it so the
+// CPU self-test exercises the same byte plans.
+RBX_HD uint32_t perm_b32(uint32_t x, uint32_t y, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(x, y, sel);
+#else
+    const uint64_t v = ((uint64_t)x << 32) | y;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = (sel >> (8 * i)) & 0xffu;
+        const uint32_t b = s < 8 ? (uint32_t)(v >> (8 * s)) & 0xffu : 0u;
+        r |= b << (8 * i);
+    }
+    return r;
+#endif
+}
+
+// zipperMerge0/1 (HighwayHash.java:248-260).  With a = lower-lane operand (Java's "v0"
+// parameter) and b = upper (Java's "v1"), byte j of the result:
+//   zm0 = [a3 b4 a2 a5 | b6 a1 b7 a0]      zm1 = [b3 a4 b2 b5 | b1 a6 b0 a7]
+// Three byte permutes each: the low word needs three source words (two perms), the high
+// word two (one perm).
 RBX_HD uint64_t zipper0(uint64_t b, uint64_t a) {
     const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bh = (uint32_t)(b >> 32);
-    const uint32_t lo = byte_of(al, 3) | (byte_of(bh, 0) << 8) | (byte_of(al, 2) << 16) | (byte_of(ah, 1) << 24);
-    const uint32_t hi = byte_of(bh, 2) | (byte_of(al, 1) << 8) | (byte_of(bh, 3) << 16) | (byte_of(al, 0) << 24);
+    const uint32_t t = perm_b32(bh, al, 0x0C020403u);   // [a3 b4 a2 0]
+    const uint32_t lo = perm_b32(ah, t, 0x05020100u);   // [a3 b4 a2 a5]
+    const uint32_t hi = perm_b32(bh, al, 0x00070106u);  // [b6 a1 b7 a0]
     return ((uint64_t)hi << 32) | lo;
 }
 
 RBX_HD uint64_t zipper1(uint64_t b, uint64_t a) {
     const uint32_t ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
-    const uint32_t lo = byte_of(bl, 3) | (byte_of(ah, 0) << 8) | (byte_of(bl, 2) << 16) | (byte_of(bh, 1) << 24);
-    const uint32_t hi = byte_of(bl, 1) | (byte_of(ah, 2) << 8) | (byte_of(bl, 0) << 16) | (byte_of(ah, 3) << 24);
+    const uint32_t t = perm_b32(ah, bl, 0x0C020403u);   // [b3 a4 b2 0]
+    const uint32_t lo = perm_b32(bh, t, 0x05020100u);   // [b3 a4 b2 b5]
+    const uint32_t hi = perm_b32(ah, bl, 0x07000601u);  // [b1 a6 b0 a7]
     return ((uint64_t)hi << 32) | lo;
 }
 
