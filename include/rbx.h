@@ -80,6 +80,14 @@ int rbx_synchronize(rbx_ctx *ctx);
 /* The context's hipStream_t, as void*. */
 void *rbx_stream(rbx_ctx *ctx);
 
+/* Pinned (page-locked) host memory for key arenas: batches whose bytes live here are
+ * uploaded by DMA at full PCIe rate (a JVM wraps it as a MemorySegment). */
+int rbx_host_alloc(uint64_t bytes, void **out);
+int rbx_host_free(void *p);
+/* Host-buffer batches are uploaded in double-buffered chunks of this many key bytes while
+ * the previous chunk computes (default 64 MiB). */
+int rbx_set_staging(rbx_ctx *ctx, uint64_t bytes);
+
 /* ---- sharding: M/connection/CRC16.java:51-57, M/cluster/ClusterConnectionManager.java:777-792 */
 uint16_t rbx_crc16(const uint8_t *bytes, size_t len);
 int rbx_calc_slot(const uint8_t *key, size_t len);

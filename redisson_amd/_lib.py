@@ -53,6 +53,9 @@ SIGNATURES = {
     "rbx_shutdown": (C.c_int, [vp]),
     "rbx_synchronize": (C.c_int, [vp]),
     "rbx_stream": (vp, [vp]),
+    "rbx_host_alloc": (C.c_int, [C.c_uint64, C.POINTER(vp)]),
+    "rbx_host_free": (C.c_int, [vp]),
+    "rbx_set_staging": (C.c_int, [vp, C.c_uint64]),
     "rbx_crc16": (C.c_uint16, [u8p, C.c_size_t]),
     "rbx_calc_slot": (C.c_int, [u8p, C.c_size_t]),
     "rbx_slot_to_gpu": (C.c_int, [C.c_int, C.c_int]),

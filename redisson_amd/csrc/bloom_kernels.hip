@@ -33,6 +33,7 @@ __device__ __forceinline__ void hash_key(const KeysDev &keys, uint64_t i, uint64
         if (keys.offsets) {
             a = keys.offsets[i];
             len = keys.offsets[i + 1] - a;
+            a -= keys.off_base;
         } else {
             a = i * keys.stride;
             len = keys.stride;

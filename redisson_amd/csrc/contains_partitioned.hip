@@ -31,6 +31,7 @@ __device__ __forceinline__ void pc_hash(const KeysDev &keys, uint64_t i, uint64_
         if (keys.offsets) {
             a = keys.offsets[i];
             len = keys.offsets[i + 1] - a;
+            a -= keys.off_base;
         } else {
             a = i * keys.stride;
             len = keys.stride;

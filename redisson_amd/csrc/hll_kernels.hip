@@ -37,6 +37,7 @@ __device__ __forceinline__ uint64_t elem_hash(const KeysDev &e, uint64_t i) {
         if (e.offsets) {
             a = e.offsets[i];
             len = e.offsets[i + 1] - a;
+            a -= e.off_base;
         } else {
             a = i * e.stride;
             len = e.stride;

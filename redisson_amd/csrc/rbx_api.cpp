@@ -198,6 +198,13 @@ struct rbx_ctx {
 
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+
+    // host-buffer pipeline: uploads on copy_stream into two device slots while the
+    // previous slot's kernels run on the compute stream
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+    DevBuf slot_bytes[2], slot_offs[2];
+    uint64_t staging_bytes = 64ull << 20;
 };
 
 static constexpr size_t kHllBytes = 16384;
@@ -641,6 +648,11 @@ int rbx_init(int device, rbx_ctx **out) {
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+        e = hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         delete c;
         return fail(RBX_E_DEVICE, hipGetErrorString(e));
@@ -661,6 +673,11 @@ int rbx_shutdown(rbx_ctx *c) {
     for (auto *p : c->hll_chunks) (void)hipFree(p);
     c->hll_chunks.clear();
     c->hll_free.clear();
+    for (int i = 0; i < 2; ++i) {
+        if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+        if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
+    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RBX_OK;
@@ -811,6 +828,54 @@ static int bitmap_for(rbx_ctx *c, const std::string &name, uint64_t size, bool c
     return RBX_OK;
 }
 
+// Runs fn(chunk view, chunk index range) over a host arena in chunks of ~staging_bytes:
+// chunk j is uploaded on copy_stream into slot j%2 while chunk j-1 computes on `st`.
+}  // extern "C"
+template <class Fn>
+static int pipelined_host_batches(rbx_ctx *c, const rbx_keys *k, hipStream_t st, Fn &&fn) {
+    uint64_t j = 0;
+    for (uint64_t i0 = 0; i0 < k->n; ++j) {
+        // chunk [i0, i1) of <= staging_bytes key bytes (at least one key)
+        uint64_t i1;
+        if (k->offsets) {
+            uint64_t lo = i0 + 1, hi = k->n;
+            const uint64_t b0 = k->offsets[i0];
+            if (k->offsets[hi] - b0 <= c->staging_bytes) {
+                lo = hi;
+            } else {
+                while (hi - lo > 0) {  // largest i1 >= i0+1 with bytes <= staging
+                    const uint64_t mid = (lo + hi + 1) / 2;
+                    if (k->offsets[mid] - b0 <= c->staging_bytes) lo = mid;
+                    else hi = mid - 1;
+                }
+            }
+            i1 = lo;
+        } else {
+            const uint64_t per = k->stride ? std::max<uint64_t>(1, c->staging_bytes / k->stride) : k->n;
+            i1 = std::min<uint64_t>(k->n, i0 + per);
+        }
+        const int s = (int)(j & 1);
+        const uint64_t n = i1 - i0;
+        const uint64_t b0 = k->offsets ? k->offsets[i0] : i0 * k->stride;
+        const uint64_t nb = k->offsets ? k->offsets[i1] - b0 : n * k->stride;
+        RBX_TRY(c->slot_bytes[s].reserve(nb + 16));
+        if (k->offsets) RBX_TRY(c->slot_offs[s].reserve((n + 1) * 8));
+        HIP_TRY(hipStreamWaitEvent(c->copy_stream, c->ev_done[s], 0));
+        if (nb) HIP_TRY(hipMemcpyAsync(c->slot_bytes[s].p, k->bytes + b0, nb, hipMemcpyHostToDevice, c->copy_stream));
+        if (k->offsets)
+            HIP_TRY(hipMemcpyAsync(c->slot_offs[s].p, k->offsets + i0, (n + 1) * 8, hipMemcpyHostToDevice, c->copy_stream));
+        HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_copied[s], 0));
+        KeysDev dk{c->slot_bytes[s].as<uint8_t>(), k->offsets ? c->slot_offs[s].as<uint64_t>() : nullptr, k->stride, n,
+                   k->offsets ? b0 : 0};
+        RBX_TRY(fn(dk, i0));
+        HIP_TRY(hipEventRecord(c->ev_done[s], st));
+        i0 = i1;
+    }
+    return RBX_OK;
+}
+extern "C" {
+
 static int bloom_host_op(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
                          uint8_t *out_flags, uint64_t *out_count, bool is_add) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx/name is NULL");
@@ -836,25 +901,19 @@ static int bloom_host_op(rbx_ctx *c, const char *name, uint64_t size, uint32_t k
     RBX_TRY(c->counters.reserve(64));
     auto *d_count = c->counters.as<unsigned long long>();
     HIP_TRY(hipMemsetAsync(d_count, 0, 8, c->stream));
-    FilterDesc f = desc_of(*bm, size, k, 0);
-    for (uint64_t i0 = 0; i0 < keys->n;) {
-        uint64_t n = std::min<uint64_t>(chunk_keys_for_upload(keys, i0), keys->n - i0);
-        KeysDev dk;
-        RBX_TRY(upload_keys(c, keys, i0, i0 + n, &dk));
-        uint8_t *d_out = nullptr;
-        if (out_flags) {
-            RBX_TRY(c->out_bytes.reserve(n));
-            d_out = c->out_bytes.as<uint8_t>();
-        }
-        if (is_add) {
-            RBX_TRY(run_add(c, dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream));
-        } else {
-            RBX_TRY(run_contains(c, dk, f, d_out, d_count, c->stream));
-        }
-        if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags + i0, d_out, n, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        i0 += n;
+    uint8_t *d_out = nullptr;
+    if (out_flags) {
+        RBX_TRY(c->out_bytes.reserve(keys->n));
+        d_out = c->out_bytes.as<uint8_t>();
     }
+    FilterDesc f = desc_of(*bm, size, k, 0);
+    HIP_TRY(hipStreamSynchronize(c->stream));  // slots may still be read by an earlier call's stream
+    RBX_TRY(pipelined_host_batches(c, keys, c->stream, [&](const KeysDev &dk, uint64_t i0) -> int {
+        uint8_t *o = d_out ? d_out + i0 : nullptr;
+        if (is_add) return run_add(c, dk, nullptr, nullptr, 0, f, k, o, d_count, nullptr, c->stream);
+        return run_contains(c, dk, f, o, d_count, c->stream);
+    }));
+    if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
     int rc;
     uint64_t cnt = read_dev_u64(c, d_count, &rc);
     RBX_TRY(rc);
@@ -1855,6 +1914,24 @@ int rbx_bench_gather_regions(rbx_ctx *c, const void *d_table, uint64_t table_byt
     launch_gather_regions((const uint32_t *)d_table, table_bytes / 4, region_bytes / 4, nlanes, (uint32_t *)d_sink,
                           pick_stream(c, stream), grid & ~7u);
     HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+int rbx_host_alloc(uint64_t bytes, void **out) {
+    if (!out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL out");
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return RBX_OK;
+}
+
+int rbx_host_free(void *p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return RBX_OK;
+}
+
+int rbx_set_staging(rbx_ctx *c, uint64_t bytes) {
+    if (!c || bytes < 4096) return fail(RBX_E_ILLEGAL_ARGUMENT, "staging must be >= 4 KiB");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    c->staging_bytes = bytes;
     return RBX_OK;
 }
 

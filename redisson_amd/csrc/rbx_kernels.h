@@ -15,6 +15,7 @@ struct KeysDev {
     const uint64_t *offsets;  // nullable: fixed stride
     uint64_t stride;
     uint64_t n;
+    uint64_t off_base;        // subtracted from offsets[] (a slice of a larger arena)
 };
 
 // One Bloom filter as the kernels see it (device-resident table for multi-tenant calls).

@@ -524,3 +524,59 @@ def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
     assert cg == cr == c2
     assert np.array_equal(pg, pr)
     f.delete()
+
+
+@pytest.mark.parametrize("staging", [4096, 65536])
+def test_host_path_pipelined_chunks(client, fresh, staging):
+    """Host-buffer batches cut into many double-buffered upload chunks (tiny staging window):
+    add order across chunks, variable-length keys split mid-arena, fixed strides."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(staging)
+    keys = [rng.bytes(int(x)) for x in rng.integers(0, 120, size=20000)]
+    keys += keys[:3000]  # duplicates in later chunks
+    mat = rng.integers(0, 256, size=(30000, 32), dtype=np.uint8)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(95850583, 7)
+    ref = O.OracleBloom(95850583, 7)
+    assert L_.lib().rbx_set_staging(client.ctx, staging) == 0
+    try:
+        cg, ng = f.addEach(Arena(keys))
+        cr, nr = ref.add(*O.arena(keys), per_key=True)
+        assert cg == cr and np.array_equal(ng, nr)
+        cg, ng = f.addEach(Arena.fixed(mat))
+        cr, nr = ref.add(*O.fixed_arena(mat), per_key=True)
+        assert cg == cr and np.array_equal(ng, nr)
+        probe = keys[::3] + [rng.bytes(int(x)) for x in rng.integers(0, 120, size=5000)]
+        cg, pg = f.containsEach(Arena(probe))
+        cr, pr = ref.contains(*O.arena(probe), per_key=True)
+        assert cg == cr and np.array_equal(pg, pr)
+    finally:
+        L_.lib().rbx_set_staging(client.ctx, 64 << 20)
+    assert f.exportBitmap() == ref.redis_string()
+    f.delete()
+
+
+def test_pinned_host_arena(client, fresh):
+    """Keys in rbx_host_alloc (pinned) memory go through the same path."""
+    import ctypes as C
+
+    from redisson_amd import _lib as L_
+    from redisson_amd.keys import Arena as A
+
+    rng = np.random.default_rng(5)
+    n, L = 50000, 16
+    p = C.c_void_p()
+    assert L_.lib().rbx_host_alloc(n * L, C.byref(p)) == 0
+    try:
+        buf = np.ctypeslib.as_array((C.c_uint8 * (n * L)).from_address(p.value))
+        buf[:] = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+        a = A.fixed(buf.reshape(n, L))
+        f = client.getBloomFilter(fresh)
+        f.tryInit(100000, 0.01)
+        ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+        assert f.add(a) == ref.add(*O.fixed_arena(buf.reshape(n, L)))
+        assert f.contains(a) == n
+        f.delete()
+    finally:
+        L_.lib().rbx_host_free(p)

@@ -74,6 +74,33 @@ def main():
                                   "gathers_per_s": lanes * 6 / (ms / 1e3)}), flush=True)
         del tb
 
+    if "hostpath" in a.what:
+        import ctypes as C
+        import time as T
+
+        import numpy as np
+
+        from redisson_amd import Arena
+        nh = 20_000_000
+        fb = client.getBloomFilter("hp")
+        fb.tryInitRaw(1 << 32, 7)
+        host = np.random.default_rng(3).integers(0, 256, size=(nh, 32), dtype=np.uint8)
+        p = C.c_void_p()
+        assert L.lib().rbx_host_alloc(nh * 32, C.byref(p)) == 0
+        pinned = np.ctypeslib.as_array((C.c_uint8 * (nh * 32)).from_address(p.value)).reshape(nh, 32)
+        pinned[:] = host
+        for label, arr in [("pageable", host), ("pinned", pinned)]:
+            a_ = Arena.fixed(arr)
+            fb.add(a_) if label == "pageable" else None
+            for _ in range(2):
+                t0 = T.perf_counter()
+                c = fb.contains(a_)
+                dt = T.perf_counter() - t0
+            print(json.dumps({"bench": "host_contains", "memory": label, "keys": nh, "s": dt,
+                              "keys_per_s": nh / dt, "present": c}), flush=True)
+        L.lib().rbx_host_free(p)
+        fb.delete()
+
     if "partition" in a.what:
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
         for name, size, k, n_add in [("C2_2^32", 1 << 32, 7, n // 2), ("C2_twin", 4294967293, 7, n // 2),
