@@ -1,29 +1,37 @@
 // contains_partitioned.hip -- RBloomFilter.contains(Collection) for one large filter
-// (M/RedissonBloomFilter.java:153-186) with region-bucketed probes.
+// (M/RedissonBloomFilter.java:153-186) with the bitmap probed from LDS instead of HBM.
 //
-// Uniformly random 4-byte gathers over a bitmap larger than the caches run at the fabric's
-// random-request rate (~55 G/s measured, flat from 64 MiB to 1 GiB), while gathers confined
-// to a 1 MiB region that one XCD keeps in its L2 run at ~130-150 G/s.  A key is absent at its
-// first 0 bit, and on a lightly filled filter most absent keys fail their first bit, so:
-//   K1 stage1 : hash every key, test bit 0 with one random gather; survivors are compacted per
-//               8192-key tile (h1, h2, key id) and their k-1 remaining bits counted per region;
-//   K2 scan   : per-region exclusive scan of the tile counts (region-major), region bases;
-//   K3 emit   : survivors' remaining bits written as (bit-in-region, key) pairs, bucketed by
-//               region (LDS cursors per tile);
-//   K4 probe  : workgroup b works on regions b%8, b%8+8, ... (an XCD's L2 holds its region --
-//               placement only affects speed); a clear bit sets the key's miss bit;
-//   K5 final  : present = survived AND NOT missed; count (+ per-key bytes).
-// The answer per key is the AND of its k bits, exactly as the direct kernel computes it.
+// Why: a uniformly random 4-byte gather that misses L2 costs one fabric request (measured
+// ~55 G requests/s chip-wide, flat from 64 MiB to 1 GiB working sets), the same request rate a
+// 128-byte streaming read gets.  A 100M-key batch issues ~4e8 such gathers into a 512 MiB bitmap
+// (4.2M cache lines), i.e. ~100 requests per line.  Routing the probes through two streaming
+// radix passes turns almost all of them into 8-byte slots of 128-byte streaming requests, and
+// the bitmap itself is read once, a 64 KiB region at a time, into LDS.
+//
+//   K1 stage1 : hash every key, test bit 0 with one random gather (a key is absent at its first
+//               0 bit, and on a lightly filled filter most absent keys fail here); survivors are
+//               compacted densely as (h1, h2, key id); `alive` bit per key.
+//   K2 emit1  : survivors' k-1 remaining bits as (bit index, key id) pairs, bucketed in LDS by
+//               coarse bucket (<= 64 buckets of 2^FB regions) and written as runs (one global
+//               reservation per bucket per flush).
+//   K3 emit2  : each coarse bucket's pairs re-bucketed by region (2^FB fine buckets).
+//   K4 probe  : one workgroup per 64 KiB region: region -> LDS, then every pair of the region
+//               tests its bit there; a clear bit sets the key's `miss` bit (rare: only keys that
+//               survived stage 1 by chance).
+//   K5 final  : present = alive AND NOT miss; count (+ per-key bytes).
+// Buckets have fixed capacities sized for "every key survives"; a pair that does not fit (only
+// for adversarial batches, e.g. one key repeated 1e8 times) is probed directly from HBM where it
+// overflows, so the answer is exact in every case.  The answer per key is the AND of its k bits,
+// exactly as the direct kernel (bloom_kernels.hip) computes it.
 #include "rbx_kernels.h"
 
 namespace rbx {
 
-constexpr int kPcTile = 8192;        // keys per K1/K3 tile
-constexpr int kPcRegionShift = 23;   // 2^23 bits = 1 MiB per region
-constexpr int kPcMaxRegions = 512;   // bitmaps up to 2^32 bits
+constexpr uint32_t kBkRegionWords = 1u << (kBkRegionBits - 5);  // 16384 words = 64 KiB
+constexpr int kBkTile2 = 8192;                                   // K3: pairs per work item (512 x 16)
 
 template <int KLEN>
-__device__ __forceinline__ void pc_hash(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
+__device__ __forceinline__ void bk_hash(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
     if constexpr (KLEN > 0) {
         hh128_fixed<KLEN>(keys.bytes + i * (uint64_t)KLEN, h1, h2);
     } else {
@@ -40,228 +48,283 @@ __device__ __forceinline__ void pc_hash(const KeysDev &keys, uint64_t i, uint64_
     }
 }
 
+// a pair whose bucket is full: test its bit in HBM
+__device__ __forceinline__ void bk_direct(unsigned long long e, const uint32_t *__restrict__ bm,
+                                          unsigned long long *__restrict__ miss) {
+    const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
+    if ((bm[idx >> 5] & bit_in_word(idx)) == 0u) atomicOr(&miss[key >> 6], 1ULL << (key & 63));
+}
+
+// Pad entry: key field 0xffffffff is never a key id (chunks hold < 2^32 keys).
+constexpr unsigned long long kBkPad = ~0ULL;
+__device__ __forceinline__ bool bk_is_pad(unsigned long long e) { return (uint32_t)e == 0xffffffffu; }
+
+// flags bit 1: runs are reserved and written in whole 128-byte lines (16 pairs), padded with
+// kBkPad, so no store covers part of a line
+__device__ __forceinline__ uint32_t bk_units(uint32_t n, uint32_t flags) { return (flags & 2) ? (n + 15u) & ~15u : n; }
+
+// writes the run s_img[st, st+n) to dst[gb, gb+units); flags bit 0: plain (L2-merged) stores
+// instead of nontemporal ones
+__device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, uint32_t st, uint32_t n, uint32_t units,
+                                             uint64_t gb, unsigned long long *__restrict__ dst, uint64_t cap,
+                                             uint32_t flags, uint32_t lane, const uint32_t *__restrict__ bm,
+                                             unsigned long long *__restrict__ miss) {
+    for (uint32_t t = lane; t < units; t += 64) {
+        const unsigned long long e = t < n ? s_img[st + t] : kBkPad;
+        const uint64_t gp = gb + t;
+        if (gp < cap) {
+            if (flags & 1) dst[gp] = e;
+            else __builtin_nontemporal_store(e, dst + gp);
+        } else if (t < n) {
+            bk_direct(e, bm, miss);
+        }
+    }
+}
+
+// exclusive scan of cnt[0..nb) (nb <= 128) by wave 0 into start[] and pos[]
+__device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t a = 2 * lane < nb ? cnt[2 * lane] : 0u;
+    const uint32_t b = 2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u;
+    uint32_t x = a + b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    const uint32_t ex = x - a - b;
+    if (2 * lane < nb) start[2 * lane] = pos[2 * lane] = ex;
+    if (2 * lane + 1 < nb) start[2 * lane + 1] = pos[2 * lane + 1] = ex + a;
+}
+
 // K1 -----------------------------------------------------------------------------------
+// Tile = 512 * PER keys.  Hash, test bit 0 (one random gather per key), then the survivors'
+// k-1 remaining bits are counted per coarse bucket in LDS, scanned, placed bucket-sorted in an
+// LDS image and written out as one run per bucket (one global reservation per bucket per tile).
+template <int KMAX> constexpr int bk_per() { return KMAX <= 8 ? 2 : 1; }
+
 template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_pc_stage1(KeysDev keys, uint64_t base, uint64_t nchunk,
+__global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                    const uint32_t *__restrict__ bm, ModParams mp, uint32_t k,
-                                                   uint4 *__restrict__ surv_h, uint32_t *__restrict__ surv_key,
-                                                   uint32_t *__restrict__ surv_cnt,
-                                                   unsigned long long *__restrict__ survive_bits,
-                                                   uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t nregions) {
-    __shared__ uint32_t s_hist[kPcMaxRegions];
-    __shared__ uint32_t s_cnt;
-    const uint32_t tile = blockIdx.x;
-    for (uint32_t r = threadIdx.x; r < nregions; r += blockDim.x) s_hist[r] = 0;
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    const uint64_t t0 = (uint64_t)tile * kPcTile;
-    const uint64_t t1 = min<uint64_t>(t0 + kPcTile, nchunk);
-    const int lane = threadIdx.x & 63;
-    for (uint64_t it = t0; it < t1; it += blockDim.x) {
-        const uint64_t t = it + threadIdx.x;
-        bool surv = false;
-        uint64_t h1 = 0, h2 = 0;
-        if (t < t1) {
-            pc_hash<KLEN>(keys, base + t, h1, h2);
-            const uint32_t idx0 = mod63(h1 & 0x7fffffffffffffffULL, mp);
-            surv = (bm[idx0 >> 5] & bit_in_word(idx0)) != 0u;
-            if (surv) {
-                uint64_t h = h1 + h2;
+                                                   uint32_t cshift, uint32_t ncoarse, uint64_t cap1,
+                                                   unsigned long long *__restrict__ pairs1, uint32_t *__restrict__ cnt1,
+                                                   unsigned long long *__restrict__ alive,
+                                                   unsigned long long *__restrict__ miss, uint32_t flags) {
+    constexpr int PER = bk_per<KMAX>();
+    constexpr int TILE = 512 * PER;
+    extern __shared__ __attribute__((aligned(16))) unsigned char bk_lds[];
+    unsigned long long *s_img = (unsigned long long *)bk_lds;  // [TILE * (KMAX-1)]
+    uint32_t *s_cnt = (uint32_t *)(s_img + TILE * (KMAX - 1));  // [128]
+    uint32_t *s_start = s_cnt + 128, *s_pos = s_start + 128, *s_gb = s_pos + 128;
+    const uint64_t ntiles = (nchunk + TILE - 1) / TILE;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
+        uint64_t h1[PER], h2[PER];
+        uint32_t w[PER], m[PER];
+        const uint64_t t0 = tile * TILE + threadIdx.x;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint64_t t = t0 + q * 512;
+            h1[q] = h2[q] = 0;
+            if (t < nchunk) bk_hash<KLEN>(keys, base + t, h1[q], h2[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint64_t t = t0 + q * 512;
+            w[q] = 0;
+            m[q] = 0;
+            if (t < nchunk) {
+                const uint32_t idx = mod63(h1[q] & 0x7fffffffffffffffULL, mp);
+                w[q] = bm[idx >> 5];
+                m[q] = bit_in_word(idx);
+            }
+        }
+        __syncthreads();  // s_cnt reset visible
+        uint32_t idx[PER][KMAX - 1];
+        bool surv[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint64_t t = t0 + q * 512;
+            surv[q] = (w[q] & m[q]) != 0u;
+            const uint64_t mask = __ballot(surv[q]);
+            if (lane == 0 && t < nchunk) alive[t >> 6] = mask;  // t is 64-aligned for lane 0
+            if (surv[q] && !(flags & 4)) {
+                uint64_t h = h1[q] + h2[q];
 #pragma unroll
                 for (int j = 1; j < KMAX; ++j) {
                     if ((uint32_t)j < k) {
-                        const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
-                        atomicAdd(&s_hist[idx >> kPcRegionShift], 1u);
+                        idx[q][j - 1] = mod63(h & 0x7fffffffffffffffULL, mp);
+                        atomicAdd(&s_cnt[idx[q][j - 1] >> cshift], 1u);
                     }
-                    h += (j & 1) ? h1 : h2;
+                    h += (j & 1) ? h1[q] : h2[q];
                 }
             }
         }
-        const uint64_t mask = __ballot(surv);
-        if (lane == 0 && t - lane < t1) survive_bits[(t - lane) >> 6] = mask;  // t - lane is 64-aligned
-        uint32_t wbase = 0;
-        if (lane == 0 && mask) wbase = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
-        wbase = __shfl(wbase, 0, 64);
-        if (surv) {
-            const uint32_t pos = wbase + (uint32_t)__popcll(mask & ((1ULL << lane) - 1));
-            surv_h[t0 + pos] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
-            surv_key[t0 + pos] = (uint32_t)t;
-        }
-    }
-    __syncthreads();
-    for (uint32_t r = threadIdx.x; r < nregions; r += blockDim.x) hist[(uint64_t)r * ntiles + tile] = s_hist[r];
-    if (threadIdx.x == 0) surv_cnt[tile] = s_cnt;
-}
-
-// K2 -----------------------------------------------------------------------------------
-// one block per region: exclusive scan of hist[r][0..ntiles) in place, row total out
-__global__ __launch_bounds__(1024) void k_pc_scan_rows(uint32_t *__restrict__ hist, uint32_t ntiles,
-                                                       unsigned long long *__restrict__ totals) {
-    __shared__ unsigned long long s_w[16];
-    uint32_t *row = hist + (uint64_t)blockIdx.x * ntiles;
-    unsigned long long carry = 0;
-    for (uint32_t c0 = 0; c0 < ntiles; c0 += blockDim.x) {
-        const uint32_t i = c0 + threadIdx.x;
-        const unsigned long long v = i < ntiles ? row[i] : 0;
-        // block-wide inclusive scan: wave scan + wave totals
-        unsigned long long x = v;
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned long long y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-        }
-        if (lane == 63) s_w[w] = x;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long acc = 0;
-            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-                const unsigned long long tq = s_w[q];
-                s_w[q] = acc;
-                acc += tq;
+        if (threadIdx.x < 64) bk_scan128(s_cnt, ncoarse, s_start, s_pos);
+        else if (threadIdx.x >= 128 && threadIdx.x - 128 < ncoarse) {
+            const uint32_t b = threadIdx.x - 128;
+            s_gb[b] = s_cnt[b] ? atomicAdd(&cnt1[b], bk_units(s_cnt[b], flags)) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (surv[q] && !(flags & 4)) {
+                const unsigned long long key = (uint32_t)(t0 + q * 512);
+#pragma unroll
+                for (int j = 1; j < KMAX; ++j) {
+                    if ((uint32_t)j < k) {
+                        const uint32_t slot = atomicAdd(&s_pos[idx[q][j - 1] >> cshift], 1u);
+                        s_img[slot] = ((unsigned long long)idx[q][j - 1] << 32) | key;
+                    }
+                }
             }
         }
         __syncthreads();
-        const unsigned long long incl = x + s_w[w];
-        if (i < ntiles) row[i] = (uint32_t)(carry + incl - v);
-        __syncthreads();
-        if (threadIdx.x == blockDim.x - 1) s_w[0] = incl;  // block total
-        __syncthreads();
-        carry += s_w[0];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
-}
-
-// single block: exclusive scan of the region totals -> region base and size
-__global__ __launch_bounds__(64) void k_pc_scan_totals(const unsigned long long *__restrict__ totals,
-                                                       uint32_t nregions, unsigned long long *__restrict__ rbase) {
-    if (threadIdx.x == 0) {
-        unsigned long long acc = 0;
-        for (uint32_t r = 0; r < nregions; ++r) {
-            rbase[r] = acc;
-            acc += totals[r];
+        for (uint32_t b = wave; b < ncoarse; b += 8) {
+            const uint32_t n = s_cnt[b];
+            bk_write_run(s_img, s_start[b], n, bk_units(n, flags), s_gb[b], pairs1 + (uint64_t)b * cap1, cap1, flags,
+                         lane, bm, miss);
         }
-        rbase[nregions] = acc;
+        __syncthreads();  // LDS reuse
     }
 }
 
 // K3 -----------------------------------------------------------------------------------
-// Sub-batches of kPcSub survivors: their (k-1) pairs are counted per region in LDS, scanned,
-// placed region-sorted into an LDS image and written out so each region's pairs of the
-// sub-batch leave as one contiguous run (coalesced stores instead of one line per pair).
-template <int KMAX> constexpr int pc_sub() { return KMAX <= 8 ? 1024 : 512; }
-
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_pc_emit(const uint4 *__restrict__ surv_h, const uint32_t *__restrict__ surv_key,
-                                                 const uint32_t *__restrict__ surv_cnt, const uint32_t *__restrict__ hist,
-                                                 const unsigned long long *__restrict__ rbase, uint32_t ntiles,
-                                                 uint32_t nregions, ModParams mp, uint32_t k,
-                                                 unsigned long long *__restrict__ pairs) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char pc_lds[];
-    unsigned long long *s_gcur = (unsigned long long *)pc_lds;                  // [512] global cursor
-    uint32_t *s_cnt = (uint32_t *)(pc_lds + kPcMaxRegions * 8);                // [512] per sub-batch
-    uint32_t *s_off = s_cnt + kPcMaxRegions;                                    // [512] scan / LDS cursor
-    constexpr int kPcSub = pc_sub<KMAX>();
-    uint32_t *s_misc = s_off + kPcMaxRegions;                                   // [4]: total
-    unsigned long long *s_img = (unsigned long long *)(s_misc + 4);            // [kPcSub * (KMAX-1)]
-    uint32_t *s_rid = (uint32_t *)(s_img + kPcSub * (KMAX - 1));               // region of each image slot
-    uint32_t &s_tot = s_misc[0];
-    const uint32_t tile = blockIdx.x;
-    for (uint32_t r = threadIdx.x; r < nregions; r += blockDim.x) s_gcur[r] = rbase[r] + hist[(uint64_t)r * ntiles + tile];
-    const uint32_t n = surv_cnt[tile];
-    const uint64_t t0 = (uint64_t)tile * kPcTile;
-    for (uint32_t s0 = 0; s0 < n; s0 += kPcSub) {
-        const uint32_t sn = min<uint32_t>(kPcSub, n - s0);
-        for (uint32_t r = threadIdx.x; r < nregions; r += blockDim.x) s_cnt[r] = 0;
+// work item = (coarse bucket c, 8192-pair tile); fine bucket = region within c.  Items are
+// numbered c-minor so the blocks running at one time reserve from different buckets' counters.
+__global__ __launch_bounds__(512) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
+                                                  const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
+                                                  uint32_t items_per_c, uint32_t fb, uint32_t nregions, uint64_t cap2,
+                                                  unsigned long long *__restrict__ pairs2, uint32_t *__restrict__ cnt2,
+                                                  const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
+                                                  uint32_t flags) {
+    constexpr int PER = kBkTile2 / 1024;  // uint4 (two pairs) per thread
+    __shared__ __attribute__((aligned(16))) unsigned long long s_img[kBkTile2];
+    __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128];
+    const uint32_t nf = 1u << fb, fmask = nf - 1;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nitems = ncoarse * items_per_c;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const uint32_t it = item / ncoarse, c = item - it * ncoarse;
+        const uint64_t nc = min<uint64_t>(cnt1[c], cap1);
+        const uint64_t start = (uint64_t)it * kBkTile2;
+        if (start >= nc) continue;  // uniform over the block
+        const uint32_t m = (uint32_t)min<uint64_t>(kBkTile2, nc - start);
+        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        // pass 1: count per region
-        for (uint32_t s = threadIdx.x; s < sn; s += blockDim.x) {
-            const uint4 hv = surv_h[t0 + s0 + s];
-            const uint64_t h1 = w2(hv.x, hv.y), h2 = w2(hv.z, hv.w);
-            uint64_t h = h1 + h2;
+        // cap1 and kBkTile2 are multiples of 64 pairs: the tile is 16-byte aligned
+        const u32x4 *src = (const u32x4 *)(pairs1 + (uint64_t)c * cap1 + start);
+        unsigned long long e[2 * PER];
 #pragma unroll
-            for (int j = 1; j < KMAX; ++j) {
-                if ((uint32_t)j < k) atomicAdd(&s_cnt[mod63(h & 0x7fffffffffffffffULL, mp) >> kPcRegionShift], 1u);
-                h += (j & 1) ? h1 : h2;
-            }
+        for (int p = 0; p < PER; ++p) {
+            const uint32_t q = 2 * (p * 512 + threadIdx.x);
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (q < m) v = __builtin_nontemporal_load(src + p * 512 + threadIdx.x);
+            e[2 * p] = w2(v.x, v.y);
+            e[2 * p + 1] = w2(v.z, v.w);
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {  // exclusive scan of <= 512 counts (cheap next to the batch)
-            uint32_t acc = 0;
-            for (uint32_t r = 0; r < nregions; ++r) {
-                s_off[r] = acc;
-                acc += s_cnt[r];
-            }
-            s_tot = acc;
-        }
-        __syncthreads();
-        // pass 2: place region-sorted in LDS
-        for (uint32_t s = threadIdx.x; s < sn; s += blockDim.x) {
-            const uint4 hv = surv_h[t0 + s0 + s];
-            const uint64_t h1 = w2(hv.x, hv.y), h2 = w2(hv.z, hv.w);
-            const unsigned long long key = surv_key[t0 + s0 + s];
-            uint64_t h = h1 + h2;
 #pragma unroll
-            for (int j = 1; j < KMAX; ++j) {
-                if ((uint32_t)j < k) {
-                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, mp);
-                    const uint32_t r = idx >> kPcRegionShift;
-                    const uint32_t slot = atomicAdd(&s_off[r], 1u);
-                    s_img[slot] = ((unsigned long long)(idx & ((1u << kPcRegionShift) - 1)) << 32) | key;
-                    s_rid[slot] = r;
-                }
-                h += (j & 1) ? h1 : h2;
+        for (int p = 0; p < 2 * PER; ++p) {
+            const uint32_t q = 2 * ((p >> 1) * 512 + threadIdx.x) + (p & 1);
+            if (q < m && !bk_is_pad(e[p])) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) bk_scan128(s_cnt, nf, s_start, s_pos);
+        else if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) {
+            const uint32_t f = threadIdx.x - 128;
+            const uint32_t r = (c << fb) + f;
+            s_gb[f] = (s_cnt[f] && r < nregions) ? atomicAdd(&cnt2[r], bk_units(s_cnt[f], flags)) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < 2 * PER; ++p) {
+            const uint32_t q = 2 * ((p >> 1) * 512 + threadIdx.x) + (p & 1);
+            if (q < m && !bk_is_pad(e[p])) {
+                const uint32_t slot = atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
+                s_img[slot] = e[p];
             }
         }
         __syncthreads();
-        // s_off[r] now = end of region r in the image; its start = end - s_cnt[r]
-        const uint32_t tot = s_tot;
-        for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
-            const uint32_t r = s_rid[q];
-            const uint32_t start = s_off[r] - s_cnt[r];
-            pairs[s_gcur[r] + (q - start)] = s_img[q];
+        for (uint32_t f = wave; f < nf; f += 8) {
+            const uint32_t n = s_cnt[f];
+            bk_write_run(s_img, s_start[f], n, bk_units(n, flags), s_gb[f], pairs2 + (uint64_t)((c << fb) + f) * cap2,
+                         cap2, flags, lane, bm, miss);
         }
-        __syncthreads();
-        for (uint32_t r = threadIdx.x; r < nregions; r += blockDim.x) s_gcur[r] += s_cnt[r];
         __syncthreads();
     }
 }
 
 // K4 -----------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pc_probe(const unsigned long long *__restrict__ pairs,
-                                                  const unsigned long long *__restrict__ rbase, uint32_t nregions,
-                                                  const uint32_t *__restrict__ bm, uint32_t *__restrict__ miss) {
-    const uint32_t xcd = blockIdx.x & 7, local = blockIdx.x >> 3, nlocal = gridDim.x >> 3;
-    for (uint32_t r = xcd; r < nregions; r += 8) {
-        const uint32_t *region = bm + ((uint64_t)r << (kPcRegionShift - 5));
-        const unsigned long long p0 = rbase[r], p1 = rbase[r + 1];
-        const unsigned long long step = (unsigned long long)nlocal * blockDim.x;
-        unsigned long long p = p0 + (unsigned long long)local * blockDim.x + threadIdx.x;
-        // 8 pairs per lane in flight
-        for (; p + 7 * step < p1; p += 8 * step) {
-            unsigned long long e[8];
-            uint32_t w[8];
+__device__ __forceinline__ void bk_test(const uint32_t *s_bm, unsigned long long e, unsigned long long *miss,
+                                        uint32_t flags) {
+    const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
+    if (key != 0xffffffffu && (s_bm[(idx & ((1u << kBkRegionBits) - 1)) >> 5] & bit_in_word(idx)) == 0u) {
+        if (flags & 8) miss[0] = 0;  // diagnostics: one fixed store instead of the scattered atomic
+        else atomicOr(&miss[key >> 6], 1ULL << (key & 63));
+    }
+}
+
+// One block per region; pairs are read as uint4 (two pairs), 8 per lane per round trip,
+// the first round issued together with the region's bitmap load.
+__global__ __launch_bounds__(1024) void k_bk_probe(const unsigned long long *__restrict__ pairs2,
+                                                   const uint32_t *__restrict__ cnt2, uint64_t cap2, uint32_t nregions,
+                                                   const uint32_t *__restrict__ bm, uint64_t nwords4,
+                                                   unsigned long long *__restrict__ miss, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
+    constexpr uint32_t NT = 1024;
+    for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+        const uint32_t n = (uint32_t)min<uint64_t>(cnt2[r], cap2);
+        if (n == 0) continue;  // uniform
+        // region bitmap (nwords4 = bitmap words rounded up to 4; the allocation covers them)
+        const uint64_t w0 = (uint64_t)r * kBkRegionWords;
+        const uint32_t nv = (uint32_t)min<uint64_t>(kBkRegionWords, nwords4 - w0) / 4;
+        const u32x4 *srcv = (const u32x4 *)(bm + w0);
+        u32x4 b[kBkRegionWords / 4 / NT];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) e[u] = __builtin_nontemporal_load(pairs + p + u * step);
+        for (uint32_t i = 0; i < kBkRegionWords / 4 / NT; ++i) {
+            const uint32_t j = i * NT + threadIdx.x;
+            if (j < nv) b[i] = srcv[j];
+        }
+        // cap2 is a multiple of 64 pairs: the region's pairs are 16-byte aligned
+        const u32x4 *src = (const u32x4 *)(pairs2 + (uint64_t)r * cap2);
+        const uint32_t n2 = (n + 1) >> 1;
+        u32x4 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[u] = region[(uint32_t)(e[u] >> 32) >> 5];
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t q = u * NT + threadIdx.x;
+            if (q < n2) v[u] = __builtin_nontemporal_load(src + q);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kBkRegionWords / 4 / NT; ++i) {
+            const uint32_t j = i * NT + threadIdx.x;
+            if (j < nv) ((u32x4 *)s_bm)[j] = b[i];
+        }
+        __syncthreads();
+        for (uint32_t base = 0;;) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const uint32_t li = (uint32_t)(e[u] >> 32), key = (uint32_t)e[u];
-                if ((w[u] & bit_in_word(li)) == 0u) atomicOr(&miss[key >> 5], 1u << (key & 31));
+                const uint32_t q = base + u * NT + threadIdx.x;
+                if (q < n2) {
+                    bk_test(s_bm, w2(v[u].x, v[u].y), miss, flags);
+                    if (2 * q + 1 < n) bk_test(s_bm, w2(v[u].z, v[u].w), miss, flags);
+                }
+            }
+            base += 8 * NT;
+            if (base >= n2) break;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t q = base + u * NT + threadIdx.x;
+                if (q < n2) v[u] = __builtin_nontemporal_load(src + q);
             }
         }
-        for (; p < p1; p += step) {
-            const unsigned long long e = pairs[p];
-            const uint32_t li = (uint32_t)(e >> 32), key = (uint32_t)e;
-            if ((region[li >> 5] & bit_in_word(li)) == 0u) atomicOr(&miss[key >> 5], 1u << (key & 31));
-        }
+        __syncthreads();  // s_bm reuse
     }
 }
 
 // K5 -----------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pc_final(const unsigned long long *__restrict__ survive_bits,
+__global__ __launch_bounds__(256) void k_bk_final(const unsigned long long *__restrict__ alive,
                                                   const unsigned long long *__restrict__ miss, uint64_t nchunk,
                                                   uint64_t base, uint8_t *__restrict__ out,
                                                   unsigned long long *__restrict__ count) {
@@ -269,14 +332,14 @@ __global__ __launch_bounds__(256) void k_pc_final(const unsigned long long *__re
     unsigned long long c = 0;
     const uint64_t ngroups = (nchunk + 63) >> 6;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += (uint64_t)gridDim.x * blockDim.x) {
-        unsigned long long pres = survive_bits[g] & ~miss[g];
+        unsigned long long pres = alive[g] & ~miss[g];
         const uint64_t rem = nchunk - (g << 6);
         if (rem < 64) pres &= (1ULL << rem) - 1;
         c += __popcll(pres);
-        if (out) {
-            const uint64_t n = rem < 64 ? rem : 64;
-            for (uint64_t b = 0; b < n; ++b) out[base + (g << 6) + b] = (pres >> b) & 1;
-        }
+    }
+    if (out) {  // one byte per key, coalesced
+        for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += (uint64_t)gridDim.x * blockDim.x)
+            out[base + t] = (uint8_t)(((alive[t >> 6] & ~miss[t >> 6]) >> (t & 63)) & 1ULL);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
@@ -290,33 +353,34 @@ __global__ __launch_bounds__(256) void k_pc_final(const unsigned long long *__re
 
 // launcher -------------------------------------------------------------------------------
 template <int KLEN, int KMAX>
-static void pc_chunk(const PcArgs &a, hipStream_t st) {
-    const uint32_t ntiles = (uint32_t)((a.nchunk + kPcTile - 1) / kPcTile);
-    hipLaunchKernelGGL((k_pc_stage1<KLEN, KMAX>), dim3(ntiles), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.bm, a.mp,
-                       a.k, a.surv_h, a.surv_key, a.surv_cnt, a.survive_bits, a.hist, ntiles, a.nregions);
-    hipLaunchKernelGGL(k_pc_scan_rows, dim3(a.nregions), dim3(1024), 0, st, a.hist, ntiles, a.totals);
-    hipLaunchKernelGGL(k_pc_scan_totals, dim3(1), dim3(64), 0, st, a.totals, a.nregions, a.rbase);
-    const size_t lds = kPcMaxRegions * 16 + 16 + (size_t)pc_sub<KMAX>() * (KMAX - 1) * 12;
-    hipLaunchKernelGGL((k_pc_emit<KMAX>), dim3(ntiles), dim3(256), lds, st, a.surv_h, a.surv_key, a.surv_cnt, a.hist,
-                       a.rbase, ntiles, a.nregions, a.mp, a.k, a.pairs);
-    hipLaunchKernelGGL(k_pc_probe, dim3(a.probe_grid), dim3(256), 0, st, a.pairs, a.rbase, a.nregions, a.bm,
-                       (uint32_t *)a.miss);
-    hipLaunchKernelGGL(k_pc_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.survive_bits, a.miss, a.nchunk,
-                       a.base, a.out, a.count);
+static void bk_chunk(const PcArgs &a, hipStream_t st) {
+    constexpr int TILE = 512 * bk_per<KMAX>();
+    const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
+    const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 2048);
+    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 4 * 128 * 4;
+    hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX>), dim3(g1), dim3(512), lds1, st, a.keys, a.base, a.nchunk, a.bm, a.mp,
+                       a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
+    const uint32_t items_per_c = (uint32_t)((a.cap1 + kBkTile2 - 1) / kBkTile2);
+    hipLaunchKernelGGL(k_bk_emit2, dim3(1024), dim3(512), 0, st, a.pairs1, a.cnt1, a.cap1, a.ncoarse, items_per_c, a.fb,
+                       a.nregions, a.cap2, a.pairs2, a.cnt2, a.bm, a.miss, a.flags);
+    hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.pairs2, a.cnt2,
+                       a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.flags);
+    hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,
+                       a.out, a.count);
 }
 
 template <int KLEN>
-static void pc_chunk_len(const PcArgs &a, hipStream_t st) {
-    if (a.k <= 8) pc_chunk<KLEN, 8>(a, st);
-    else pc_chunk<KLEN, 16>(a, st);
+static void bk_chunk_len(const PcArgs &a, hipStream_t st) {
+    if (a.k <= 8) bk_chunk<KLEN, 8>(a, st);
+    else bk_chunk<KLEN, 16>(a, st);
 }
 
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st) {
     switch (klen_fast) {
-    case 16: pc_chunk_len<16>(a, st); break;
-    case 32: pc_chunk_len<32>(a, st); break;
-    case 64: pc_chunk_len<64>(a, st); break;
-    default: pc_chunk_len<0>(a, st); break;
+    case 16: bk_chunk_len<16>(a, st); break;
+    case 32: bk_chunk_len<32>(a, st); break;
+    case 64: bk_chunk_len<64>(a, st); break;
+    default: bk_chunk_len<0>(a, st); break;
     }
 }
 

@@ -183,7 +183,7 @@ struct rbx_ctx {
 
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
-    DevBuf pc_surv_h, pc_surv_key, pc_surv_cnt, pc_bits, pc_hist, pc_scan, pc_pairs;  // partitioned contains
+    DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2;  // partitioned contains
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
@@ -546,34 +546,47 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
 }
 
 // Partitioned contains (contains_partitioned.hip) for one large filter.  Mode: 0 never,
-// 1 whenever k in [2, 16], 2 when the bitmap exceeds 16 MiB and the batch >= 1M keys.  Default 0:
-// on MI355X the direct early-exit kernel is faster (DESIGN.md §3.6 has the measurements).
-static int g_partition_mode = 0;
+// 1 whenever k in [2, 16], 2 (default) when the bitmap is >= 64 MiB and the batch >= 4M keys:
+// there the random-gather rate binds the direct kernel (DESIGN.md §3.6 has the measurements).
+static int g_partition_mode = 2;
+static int g_partition_flags = 0;
 
 static bool use_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 2 || k > 16 || size > (1ULL << 32)) return false;
     if (g_partition_mode == 0) return false;
     if (g_partition_mode == 1) return true;
-    return size > (128ULL << 20) && n >= (1ULL << 20);
+    return size >= (1ULL << 29) && n >= (1ULL << 22);
 }
 
 static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,
                                     unsigned long long *d_count, hipStream_t st) {
     const uint32_t k = f.k;
-    const uint32_t nregions = (uint32_t)((f.mp.size + (1ULL << kPcRegionBits) - 1) >> kPcRegionBits);
+    const uint64_t size = f.mp.size;
+    const uint32_t nregions = (uint32_t)((size + (1ULL << kBkRegionBits) - 1) >> kBkRegionBits);
+    uint32_t lg = 0;
+    while ((1ULL << lg) < nregions) ++lg;
+    const uint32_t fb = lg > 6 ? lg - 6 : 0;
+    const uint32_t ncoarse = (nregions + (1u << fb) - 1) >> fb;
+    // keys per chunk: key ids fit 32 bits and a chunk's pairs stay <= 2^30
     uint64_t chunk = std::min<uint64_t>(1ULL << 27, (1ULL << 30) / (k - 1));
     const uint64_t nch = (keys.n + chunk - 1) / chunk;
     chunk = (keys.n + nch - 1) / nch;
-    chunk = (chunk + kPcTileKeys - 1) / kPcTileKeys * kPcTileKeys;
-    const uint64_t ntiles = chunk / kPcTileKeys;
+    chunk = (chunk + 1023) / 1024 * 1024;
     const uint64_t ngroups = (chunk + 63) / 64;
-    RBX_TRY(c->pc_surv_h.reserve(chunk * 16));
-    RBX_TRY(c->pc_surv_key.reserve(chunk * 4));
-    RBX_TRY(c->pc_surv_cnt.reserve(ntiles * 4));
+    // capacities assume every key survives stage 1; pairs spread uniformly over [0, size)
+    const double pairs_max = (double)chunk * (k - 1);
+    const double frac1 = std::min(1.0, (double)(1ULL << (kBkRegionBits + fb)) / (double)size);
+    const double frac2 = std::min(1.0, (double)(1ULL << kBkRegionBits) / (double)size);
+    // (+ room for the padding of 128-byte aligned runs: <= 15 pairs per run)
+    uint64_t cap1 = (uint64_t)(pairs_max * frac1 * 1.25) + 16384;
+    uint64_t cap2 = (uint64_t)(pairs_max * frac2 * 1.35) + 4096;
+    cap1 = (cap1 + 63) / 64 * 64;
+    cap2 = (cap2 + 63) / 64 * 64;
     RBX_TRY(c->pc_bits.reserve(ngroups * 16));
-    RBX_TRY(c->pc_hist.reserve((uint64_t)nregions * ntiles * 4));
-    RBX_TRY(c->pc_scan.reserve((2 * (uint64_t)nregions + 1) * 8));
-    RBX_TRY(c->pc_pairs.reserve(chunk * (k - 1) * 8));
+    const uint64_t ncnt = 64 + (uint64_t)nregions;  // cnt1 (padded to 64), cnt2
+    RBX_TRY(c->pc_cnt.reserve(ncnt * 4));
+    RBX_TRY(c->pc_pairs1.reserve((uint64_t)ncoarse * cap1 * 8));
+    RBX_TRY(c->pc_pairs2.reserve((uint64_t)nregions * cap2 * 8));
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         PcArgs a{};
@@ -584,19 +597,23 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
         a.mp = f.mp;
         a.k = k;
         a.nregions = nregions;
-        a.surv_h = c->pc_surv_h.as<uint4>();
-        a.surv_key = c->pc_surv_key.as<uint32_t>();
-        a.surv_cnt = c->pc_surv_cnt.as<uint32_t>();
-        a.survive_bits = c->pc_bits.as<unsigned long long>();
-        a.miss = a.survive_bits + ngroups;
-        a.hist = c->pc_hist.as<uint32_t>();
-        a.totals = c->pc_scan.as<unsigned long long>();
-        a.rbase = a.totals + nregions;
-        a.pairs = c->pc_pairs.as<unsigned long long>();
-        a.probe_grid = 2048;
+        a.fb = fb;
+        a.cshift = kBkRegionBits + fb;
+        a.ncoarse = ncoarse;
+        a.cap1 = cap1;
+        a.cap2 = cap2;
+        a.nwords4 = (size + 127) / 128 * 4;
+        a.alive = c->pc_bits.as<unsigned long long>();
+        a.miss = a.alive + ngroups;
+        a.cnt1 = c->pc_cnt.as<uint32_t>();
+        a.cnt2 = a.cnt1 + 64;
+        a.pairs1 = c->pc_pairs1.as<unsigned long long>();
+        a.pairs2 = c->pc_pairs2.as<unsigned long long>();
         a.out = d_out;
         a.count = d_count;
+        a.flags = (uint32_t)g_partition_flags;
         HIP_TRY(hipMemsetAsync(a.miss, 0, ngroups * 8, st));
+        HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
         launch_contains_partitioned_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
     }
@@ -1941,6 +1958,13 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "contains_partition")) {
         if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition in [0, 2]");
         g_partition_mode = value;
+        return RBX_OK;
+    }
+    // bits 0-1: store variants (results unchanged); bits 2-3: DIAGNOSTICS ONLY, results become
+    // wrong (4: stage 1 emits no pairs; 8: the probe records no misses) -- microbench timing
+    if (!strcmp(key, "contains_partition_flags")) {
+        if (value < 0 || value > 15) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in [0, 15]");
+        g_partition_flags = value;
         return RBX_OK;
     }
     if (!strcmp(key, "contains_stage1")) {

@@ -51,28 +51,29 @@ struct AddChunkArgs {
 };
 
 // partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
+constexpr int kBkRegionBits = 19;  // 2^19 bits = 64 KiB bitmap region = one LDS image
 struct PcArgs {
     KeysDev keys;
     uint64_t base, nchunk;
     const uint32_t *bm;
     ModParams mp;
     uint32_t k;
-    uint32_t nregions;      // ceil(size / 2^23)
-    uint4 *surv_h;          // nchunk records
-    uint32_t *surv_key;     // nchunk
-    uint32_t *surv_cnt;     // per tile
-    unsigned long long *survive_bits;  // ceil(nchunk/64)
-    unsigned long long *miss;          // ceil(nchunk/64), zeroed
-    uint32_t *hist;         // nregions x ntiles
-    unsigned long long *totals;        // nregions
-    unsigned long long *rbase;         // nregions + 1
-    unsigned long long *pairs;         // <= (k-1) * nchunk
-    unsigned probe_grid;
+    uint32_t nregions;      // ceil(size / 2^kBkRegionBits)
+    uint32_t fb;            // regions per coarse bucket = 2^fb
+    uint32_t cshift;        // kBkRegionBits + fb
+    uint32_t ncoarse;       // <= 64
+    uint64_t cap1, cap2;    // pair capacity per coarse bucket / per region
+    uint64_t nwords4;       // bitmap words rounded up to a multiple of 4
+    uint32_t *cnt1;         // ncoarse, zeroed
+    uint32_t *cnt2;         // nregions, zeroed
+    unsigned long long *alive;  // ceil(nchunk/64)
+    unsigned long long *miss;   // ceil(nchunk/64), zeroed
+    unsigned long long *pairs1; // ncoarse * cap1
+    unsigned long long *pairs2; // nregions * cap2
     uint8_t *out;
     unsigned long long *count;
+    uint32_t flags;  // bit 0: plain stores for pair runs; bit 1: 128-byte aligned padded runs
 };
-constexpr uint64_t kPcTileKeys = 8192;
-constexpr uint32_t kPcRegionBits = 23;
 inline unsigned grid_for_pc(uint64_t n) {
     uint64_t g = ((n + 63) / 64 + 255) / 256;
     return (unsigned)(g < 1 ? 1 : (g > 2048 ? 2048 : g));

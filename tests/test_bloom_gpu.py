@@ -357,10 +357,12 @@ def test_device_path_matches_host_path(client, fresh):
 
 
 def test_full_size_2pow32_property(client, fresh):
-    """C2 geometry (m = 2^32, k = 7) at 4M 32-byte keys: add counts and per-key flags equal the
-    oracle, no false negatives, false-positive rate near theory, bitmap bytes identical."""
+    """C2 geometry (m = 2^32, k = 7) at 4.2M 32-byte keys (above the 2^22-key threshold of the
+    default partitioned contains): add counts and per-key flags equal the oracle, no false
+    negatives, false-positive rate near theory, per-key contains flags of fresh keys equal the
+    oracle's, bitmap bytes identical."""
     rng = np.random.default_rng(0x5EED0002)
-    n = 4_000_000
+    n = 4_200_000
     mat = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     f = client.getBloomFilter(fresh)
     f.tryInitRaw(1 << 32, 7)
@@ -370,11 +372,41 @@ def test_full_size_2pow32_property(client, fresh):
     cr, nr = ref.add(*O.fixed_arena(mat), per_key=True)
     assert cg == cr == n and np.array_equal(ng, nr)
     assert f.contains(a) == n
-    fresh_keys = Arena.fixed(rng.integers(0, 256, size=(n, 32), dtype=np.uint8))
-    fp = f.contains(fresh_keys)
+    fmat = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    fp, pg = f.containsEach(Arena.fixed(fmat))
     theory = (1 - np.exp(-7 * n / 2**32)) ** 7
     assert fp <= max(10, 5 * theory * n)
+    cr, pr = ref.contains(*O.fixed_arena(fmat), per_key=True)
+    assert fp == cr and np.array_equal(pg, pr)
     assert f.exportBitmap() == ref.redis_string()
+    f.delete()
+
+
+@pytest.mark.parametrize("mode", [1, 5, 7])
+def test_partitioned_contains_bucket_overflow(client, fresh, mode):
+    """Batches that overflow the partitioned path's fixed bucket capacities (a few keys repeated
+    hundreds of thousands of times put all pairs into k-1 buckets): the overflowing pairs are
+    probed directly and every per-key answer still equals the oracle's."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(77)
+    base = rng.integers(0, 256, size=(40, 32), dtype=np.uint8)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 30, 7)
+    ref = O.OracleBloom(1 << 30, 7)
+    f.add(Arena.fixed(base[:20]))
+    ref.add(*O.fixed_arena(base[:20]))
+    probe = np.concatenate([base[rng.integers(0, 40, size=400_000)], rng.integers(0, 256, size=(50_000, 32),
+                                                                                 dtype=np.uint8)])
+    assert L_.lib().rbx_tune(b"contains_partition", 1) == 0
+    assert L_.lib().rbx_tune(b"contains_partition_flags", mode >> 1) == 0
+    try:
+        cg, pg = f.containsEach(Arena.fixed(probe))
+    finally:
+        L_.lib().rbx_tune(b"contains_partition", 2)
+        L_.lib().rbx_tune(b"contains_partition_flags", 0)
+    cr, pr = ref.contains(*O.fixed_arena(probe), per_key=True)
+    assert cg == cr and np.array_equal(pg, pr)
     f.delete()
 
 
@@ -491,7 +523,7 @@ def test_mixed_stream_in_order_semantics(client, fresh, seed):
         client.getBloomFilter(n).delete()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 5, 7])
 @pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
                                       (14377587, 2, 64), (95850583, 16, 0), (8388608 * 3 + 5, 5, 24)])
 def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
@@ -514,12 +546,14 @@ def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
     ref = O.OracleBloom(size, k)
     f.add(a_add)
     ref.add(*o_add)
-    assert L_.lib().rbx_tune(b"contains_partition", mode) == 0
+    assert L_.lib().rbx_tune(b"contains_partition", min(mode, 1)) == 0
+    assert L_.lib().rbx_tune(b"contains_partition_flags", mode >> 1) == 0  # 5: plain stores, 7: + aligned runs
     try:
         cg, pg = f.containsEach(a_probe)
         c2 = f.contains(a_probe)
     finally:
-        L_.lib().rbx_tune(b"contains_partition", 0)
+        L_.lib().rbx_tune(b"contains_partition", 2)
+        L_.lib().rbx_tune(b"contains_partition_flags", 0)
     cr, pr = ref.contains(*o_probe, per_key=True)
     assert cg == cr == c2
     assert np.array_equal(pg, pr)

@@ -125,9 +125,39 @@ def main():
                 print(json.dumps({"bench": "contains_partition", "filter": name, "mode": mode, "ms_median": med,
                                   "ms_min": min(v), "keys_per_s": n / (med / 1e3), "present_x2": counts[mode]}),
                       flush=True)
-            L.lib().rbx_tune(b"contains_partition", 0)
+            L.lib().rbx_tune(b"contains_partition", 2)
             h.close()
             fb.delete()
+
+    if "pflags" in a.what:
+        # partitioned contains store variants (rbx_tune contains_partition_flags) vs direct
+        cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+        fb = client.getBloomFilter("pf-C2")
+        fb.tryInitRaw(1 << 32, 7)
+        h = BloomHandle(client, "pf-C2")
+        h.add_dev(device_keys(keys.data_ptr(), n // 2, 32), cnt.data_ptr(), stream=sp)
+        torch.cuda.synchronize()
+        dk = device_keys(keys.data_ptr(), n, 32)
+        variants = [(0, 0)] + [(1, fl) for fl in range(4)] + [(1, 4), (1, 8)]  # 4, 8: diagnostics
+        res = {v: [] for v in variants}
+        counts = {}
+        for rnd in range(5):
+            for mode, fl in variants:
+                L.lib().rbx_tune(b"contains_partition", mode)
+                L.lib().rbx_tune(b"contains_partition_flags", fl)
+                cnt[1].zero_()
+                res[(mode, fl)].append(timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 8, stream=sp), 2))
+                if fl < 4:
+                    counts[(mode, fl)] = int(cnt[1].item())
+        assert len(set(counts.values())) == 1, counts
+        for (mode, fl), v in res.items():
+            med = statistics.median(v)
+            print(json.dumps({"bench": "contains_pflags", "mode": mode, "flags": fl, "ms_median": med,
+                              "keys_per_s": n / (med / 1e3)}), flush=True)
+        L.lib().rbx_tune(b"contains_partition", 2)
+        L.lib().rbx_tune(b"contains_partition_flags", 0)
+        h.close()
+        fb.delete()
 
     if "stage1" in a.what or "sizes" in a.what:
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
