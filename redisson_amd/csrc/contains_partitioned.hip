@@ -9,16 +9,19 @@
 // the bitmap itself is read once, a 64 KiB region at a time, into LDS.
 //
 //   K1 stage1 : hash every key, test bit 0 with one random gather (a key is absent at its first
-//               0 bit, and on a lightly filled filter most absent keys fail here); survivors are
-//               compacted densely as (h1, h2, key id); `alive` bit per key.
-//   K2 emit1  : survivors' k-1 remaining bits as (bit index, key id) pairs, bucketed in LDS by
-//               coarse bucket (<= 64 buckets of 2^FB regions) and written as runs (one global
-//               reservation per bucket per flush).
+//               0 bit, and on a lightly filled filter most absent keys fail here); `alive` bit per
+//               key; the survivors' k-1 remaining bits become (bit index, key id) pairs, bucketed
+//               in LDS by coarse bucket (<= 64 buckets of 2^FB regions, each split into kBkSub
+//               sub-partitions with their own counters) and written as runs.
 //   K3 emit2  : each coarse bucket's pairs re-bucketed by region (2^FB fine buckets).
 //   K4 probe  : one workgroup per 64 KiB region: region -> LDS, then every pair of the region
 //               tests its bit there; a clear bit sets the key's `miss` bit (rare: only keys that
 //               survived stage 1 by chance).
 //   K5 final  : present = alive AND NOT miss; count (+ per-key bytes).
+// Measured bound (rocprof PMC, C2): every kernel runs at ~50 G memory requests/s at the L2->EA
+// interface (a read moves 128 B, a write 64 B, an atomic is one request), the same rate the
+// direct kernel's random gathers get; this path issues ~2.8e8 requests per 1e8 keys where the
+// direct kernel issues ~4.4e8.
 // Buckets have fixed capacities sized for "every key survives"; a pair that does not fit (only
 // for adversarial batches, e.g. one key repeated 1e8 times) is probed directly from HBM where it
 // overflows, so the answer is exact in every case.  The answer per key is the AND of its k bits,
@@ -28,7 +31,9 @@
 namespace rbx {
 
 constexpr uint32_t kBkRegionWords = 1u << (kBkRegionBits - 5);  // 16384 words = 64 KiB
-constexpr int kBkTile2 = 8192;                                   // K3: pairs per work item (512 x 16)
+// Each coarse bucket is split into kBkSub sub-partitions with their own reservation counters;
+// stage-1 block b writes to sub-partition b % kBkSub (one counter per bucket would take every
+// block's reservation: ~1e5 same-address atomics per counter per 1e8 keys).
 
 template <int KLEN>
 __device__ __forceinline__ void bk_hash(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
@@ -55,29 +60,15 @@ __device__ __forceinline__ void bk_direct(unsigned long long e, const uint32_t *
     if ((bm[idx >> 5] & bit_in_word(idx)) == 0u) atomicOr(&miss[key >> 6], 1ULL << (key & 63));
 }
 
-// Pad entry: key field 0xffffffff is never a key id (chunks hold < 2^32 keys).
-constexpr unsigned long long kBkPad = ~0ULL;
-__device__ __forceinline__ bool bk_is_pad(unsigned long long e) { return (uint32_t)e == 0xffffffffu; }
-
-// flags bit 1: runs are reserved and written in whole 128-byte lines (16 pairs), padded with
-// kBkPad, so no store covers part of a line
-__device__ __forceinline__ uint32_t bk_units(uint32_t n, uint32_t flags) { return (flags & 2) ? (n + 15u) & ~15u : n; }
-
-// writes the run s_img[st, st+n) to dst[gb, gb+units); flags bit 0: plain (L2-merged) stores
-// instead of nontemporal ones
-__device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, uint32_t st, uint32_t n, uint32_t units,
-                                             uint64_t gb, unsigned long long *__restrict__ dst, uint64_t cap,
-                                             uint32_t flags, uint32_t lane, const uint32_t *__restrict__ bm,
-                                             unsigned long long *__restrict__ miss) {
-    for (uint32_t t = lane; t < units; t += 64) {
-        const unsigned long long e = t < n ? s_img[st + t] : kBkPad;
+// writes the run s_img[st, st+n) to dst[gb, gb+n); pairs past the capacity are probed directly
+__device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, uint32_t st, uint32_t n, uint64_t gb,
+                                             unsigned long long *__restrict__ dst, uint64_t cap, uint32_t lane,
+                                             const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss) {
+    for (uint32_t t = lane; t < n; t += 64) {
+        const unsigned long long e = s_img[st + t];
         const uint64_t gp = gb + t;
-        if (gp < cap) {
-            if (flags & 1) dst[gp] = e;
-            else __builtin_nontemporal_store(e, dst + gp);
-        } else if (t < n) {
-            bk_direct(e, bm, miss);
-        }
+        if (gp < cap) __builtin_nontemporal_store(e, dst + gp);
+        else bk_direct(e, bm, miss);
     }
 }
 
@@ -98,26 +89,27 @@ __device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uin
 }
 
 // K1 -----------------------------------------------------------------------------------
-// Tile = 512 * PER keys.  Hash, test bit 0 (one random gather per key), then the survivors'
+// Tile = NT * PER keys.  Hash, test bit 0 (one random gather per key), then the survivors'
 // k-1 remaining bits are counted per coarse bucket in LDS, scanned, placed bucket-sorted in an
 // LDS image and written out as one run per bucket (one global reservation per bucket per tile).
 template <int KMAX> constexpr int bk_per() { return KMAX <= 8 ? 2 : 1; }
 
-template <int KLEN, int KMAX>
-__global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, uint64_t nchunk,
+template <int KLEN, int KMAX, int NT>
+__global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                    const uint32_t *__restrict__ bm, ModParams mp, uint32_t k,
                                                    uint32_t cshift, uint32_t ncoarse, uint64_t cap1,
                                                    unsigned long long *__restrict__ pairs1, uint32_t *__restrict__ cnt1,
                                                    unsigned long long *__restrict__ alive,
                                                    unsigned long long *__restrict__ miss, uint32_t flags) {
     constexpr int PER = bk_per<KMAX>();
-    constexpr int TILE = 512 * PER;
+    constexpr int TILE = NT * PER;
     extern __shared__ __attribute__((aligned(16))) unsigned char bk_lds[];
     unsigned long long *s_img = (unsigned long long *)bk_lds;  // [TILE * (KMAX-1)]
     uint32_t *s_cnt = (uint32_t *)(s_img + TILE * (KMAX - 1));  // [128]
     uint32_t *s_start = s_cnt + 128, *s_pos = s_start + 128, *s_gb = s_pos + 128;
     const uint64_t ntiles = (nchunk + TILE - 1) / TILE;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t sub = blockIdx.x % kBkSub;
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         uint64_t h1[PER], h2[PER];
@@ -125,13 +117,13 @@ __global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, 
         const uint64_t t0 = tile * TILE + threadIdx.x;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const uint64_t t = t0 + q * 512;
+            const uint64_t t = t0 + q * NT;
             h1[q] = h2[q] = 0;
             if (t < nchunk) bk_hash<KLEN>(keys, base + t, h1[q], h2[q]);
         }
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const uint64_t t = t0 + q * 512;
+            const uint64_t t = t0 + q * NT;
             w[q] = 0;
             m[q] = 0;
             if (t < nchunk) {
@@ -145,7 +137,7 @@ __global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, 
         bool surv[PER];
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const uint64_t t = t0 + q * 512;
+            const uint64_t t = t0 + q * NT;
             surv[q] = (w[q] & m[q]) != 0u;
             const uint64_t mask = __ballot(surv[q]);
             if (lane == 0 && t < nchunk) alive[t >> 6] = mask;  // t is 64-aligned for lane 0
@@ -165,13 +157,13 @@ __global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, 
         if (threadIdx.x < 64) bk_scan128(s_cnt, ncoarse, s_start, s_pos);
         else if (threadIdx.x >= 128 && threadIdx.x - 128 < ncoarse) {
             const uint32_t b = threadIdx.x - 128;
-            s_gb[b] = s_cnt[b] ? atomicAdd(&cnt1[b], bk_units(s_cnt[b], flags)) : 0u;
+            s_gb[b] = s_cnt[b] ? atomicAdd(&cnt1[b * kBkSub + sub], s_cnt[b]) : 0u;
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             if (surv[q] && !(flags & 4)) {
-                const unsigned long long key = (uint32_t)(t0 + q * 512);
+                const unsigned long long key = (uint32_t)(t0 + q * NT);
 #pragma unroll
                 for (int j = 1; j < KMAX; ++j) {
                     if ((uint32_t)j < k) {
@@ -182,10 +174,10 @@ __global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, 
             }
         }
         __syncthreads();
-        for (uint32_t b = wave; b < ncoarse; b += 8) {
+        for (uint32_t b = wave; b < ncoarse; b += NT / 64) {
             const uint32_t n = s_cnt[b];
-            bk_write_run(s_img, s_start[b], n, bk_units(n, flags), s_gb[b], pairs1 + (uint64_t)b * cap1, cap1, flags,
-                         lane, bm, miss);
+            bk_write_run(s_img, s_start[b], n, s_gb[b], pairs1 + (uint64_t)(b * kBkSub + sub) * cap1, cap1, lane, bm,
+                         miss);
         }
         __syncthreads();  // LDS reuse
     }
@@ -194,63 +186,68 @@ __global__ __launch_bounds__(512) void k_bk_stage1(KeysDev keys, uint64_t base, 
 // K3 -----------------------------------------------------------------------------------
 // work item = (coarse bucket c, 8192-pair tile); fine bucket = region within c.  Items are
 // numbered c-minor so the blocks running at one time reserve from different buckets' counters.
-__global__ __launch_bounds__(512) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
                                                   const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
                                                   uint32_t items_per_c, uint32_t fb, uint32_t nregions, uint64_t cap2,
                                                   unsigned long long *__restrict__ pairs2, uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
                                                   uint32_t flags) {
-    constexpr int PER = kBkTile2 / 1024;  // uint4 (two pairs) per thread
-    __shared__ __attribute__((aligned(16))) unsigned long long s_img[kBkTile2];
+    constexpr int PER = 8;  // uint4 (two pairs) per thread
+    constexpr int TILE = 16 * NT;
+    __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
     __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128];
     const uint32_t nf = 1u << fb, fmask = nf - 1;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t nitems = ncoarse * items_per_c;
+    const uint32_t nparts = ncoarse * kBkSub;
+    const uint32_t nitems = nparts * items_per_c;
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const uint32_t it = item / ncoarse, c = item - it * ncoarse;
-        const uint64_t nc = min<uint64_t>(cnt1[c], cap1);
-        const uint64_t start = (uint64_t)it * kBkTile2;
+        // c-minor: the blocks resident at one time spread over all coarse buckets (and so over
+        // different regions' counters)
+        const uint32_t it = item / nparts, ix = item - it * nparts;
+        const uint32_t c = ix % ncoarse, cs = c * kBkSub + ix / ncoarse;
+        const uint64_t nc = min<uint64_t>(cnt1[cs], cap1);
+        const uint64_t start = (uint64_t)it * TILE;
         if (start >= nc) continue;  // uniform over the block
-        const uint32_t m = (uint32_t)min<uint64_t>(kBkTile2, nc - start);
+        const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
         if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        // cap1 and kBkTile2 are multiples of 64 pairs: the tile is 16-byte aligned
-        const u32x4 *src = (const u32x4 *)(pairs1 + (uint64_t)c * cap1 + start);
+        // cap1 and TILE are multiples of 64 pairs: the tile is 16-byte aligned
+        const u32x4 *src = (const u32x4 *)(pairs1 + (uint64_t)cs * cap1 + start);
         unsigned long long e[2 * PER];
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
-            const uint32_t q = 2 * (p * 512 + threadIdx.x);
+            const uint32_t q = 2 * (p * NT + threadIdx.x);
             u32x4 v = {0u, 0u, 0u, 0u};
-            if (q < m) v = __builtin_nontemporal_load(src + p * 512 + threadIdx.x);
+            if (q < m) v = __builtin_nontemporal_load(src + p * NT + threadIdx.x);
             e[2 * p] = w2(v.x, v.y);
             e[2 * p + 1] = w2(v.z, v.w);
         }
 #pragma unroll
         for (int p = 0; p < 2 * PER; ++p) {
-            const uint32_t q = 2 * ((p >> 1) * 512 + threadIdx.x) + (p & 1);
-            if (q < m && !bk_is_pad(e[p])) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
+            const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+            if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
         }
         __syncthreads();
         if (threadIdx.x < 64) bk_scan128(s_cnt, nf, s_start, s_pos);
         else if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) {
             const uint32_t f = threadIdx.x - 128;
             const uint32_t r = (c << fb) + f;
-            s_gb[f] = (s_cnt[f] && r < nregions) ? atomicAdd(&cnt2[r], bk_units(s_cnt[f], flags)) : 0u;
+            s_gb[f] = (s_cnt[f] && r < nregions) ? atomicAdd(&cnt2[r], s_cnt[f]) : 0u;
         }
         __syncthreads();
 #pragma unroll
         for (int p = 0; p < 2 * PER; ++p) {
-            const uint32_t q = 2 * ((p >> 1) * 512 + threadIdx.x) + (p & 1);
-            if (q < m && !bk_is_pad(e[p])) {
+            const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+            if (q < m) {
                 const uint32_t slot = atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
                 s_img[slot] = e[p];
             }
         }
         __syncthreads();
-        for (uint32_t f = wave; f < nf; f += 8) {
+        for (uint32_t f = wave; f < nf; f += NT / 64) {
             const uint32_t n = s_cnt[f];
-            bk_write_run(s_img, s_start[f], n, bk_units(n, flags), s_gb[f], pairs2 + (uint64_t)((c << fb) + f) * cap2,
-                         cap2, flags, lane, bm, miss);
+            bk_write_run(s_img, s_start[f], n, s_gb[f], pairs2 + (uint64_t)((c << fb) + f) * cap2, cap2, lane, bm, miss);
         }
         __syncthreads();
     }
@@ -260,7 +257,7 @@ __global__ __launch_bounds__(512) void k_bk_emit2(const unsigned long long *__re
 __device__ __forceinline__ void bk_test(const uint32_t *s_bm, unsigned long long e, unsigned long long *miss,
                                         uint32_t flags) {
     const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
-    if (key != 0xffffffffu && (s_bm[(idx & ((1u << kBkRegionBits) - 1)) >> 5] & bit_in_word(idx)) == 0u) {
+    if ((s_bm[(idx & ((1u << kBkRegionBits) - 1)) >> 5] & bit_in_word(idx)) == 0u) {
         if (flags & 8) miss[0] = 0;  // diagnostics: one fixed store instead of the scattered atomic
         else atomicOr(&miss[key >> 6], 1ULL << (key & 63));
     }
@@ -352,17 +349,28 @@ __global__ __launch_bounds__(256) void k_bk_final(const unsigned long long *__re
 }
 
 // launcher -------------------------------------------------------------------------------
+template <int KLEN, int KMAX, int NT1>
+static void bk_stage1(const PcArgs &a, hipStream_t st) {
+    constexpr int TILE = NT1 * bk_per<KMAX>();
+    const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
+    const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 4096);
+    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 4 * 128 * 4;
+    hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX, NT1>), dim3(g1), dim3(NT1), lds1, st, a.keys, a.base, a.nchunk, a.bm,
+                       a.mp, a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
+}
+
+template <int NT2>
+static void bk_emit2(const PcArgs &a, hipStream_t st) {
+    // cap1 is a multiple of 64 pairs and of every tile size used here (>= 16 * 256)
+    const uint32_t items_per_c = (uint32_t)((a.cap1 + 16 * NT2 - 1) / (16 * NT2));
+    hipLaunchKernelGGL((k_bk_emit2<NT2>), dim3(2048), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1, a.ncoarse,
+                       items_per_c, a.fb, a.nregions, a.cap2, a.pairs2, a.cnt2, a.bm, a.miss, a.flags);
+}
+
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
-    constexpr int TILE = 512 * bk_per<KMAX>();
-    const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
-    const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 2048);
-    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 4 * 128 * 4;
-    hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX>), dim3(g1), dim3(512), lds1, st, a.keys, a.base, a.nchunk, a.bm, a.mp,
-                       a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
-    const uint32_t items_per_c = (uint32_t)((a.cap1 + kBkTile2 - 1) / kBkTile2);
-    hipLaunchKernelGGL(k_bk_emit2, dim3(1024), dim3(512), 0, st, a.pairs1, a.cnt1, a.cap1, a.ncoarse, items_per_c, a.fb,
-                       a.nregions, a.cap2, a.pairs2, a.cnt2, a.bm, a.miss, a.flags);
+    bk_stage1<KLEN, KMAX, 512>(a, st);
+    bk_emit2<512>(a, st);
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.pairs2, a.cnt2,
                        a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.flags);
     hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,

@@ -577,15 +577,14 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
     const double pairs_max = (double)chunk * (k - 1);
     const double frac1 = std::min(1.0, (double)(1ULL << (kBkRegionBits + fb)) / (double)size);
     const double frac2 = std::min(1.0, (double)(1ULL << kBkRegionBits) / (double)size);
-    // (+ room for the padding of 128-byte aligned runs: <= 15 pairs per run)
-    uint64_t cap1 = (uint64_t)(pairs_max * frac1 * 1.25) + 16384;
-    uint64_t cap2 = (uint64_t)(pairs_max * frac2 * 1.35) + 4096;
-    cap1 = (cap1 + 63) / 64 * 64;
+    uint64_t cap1 = (uint64_t)(pairs_max * frac1 / kBkSub * 1.15) + 8192;
+    uint64_t cap2 = (uint64_t)(pairs_max * frac2 * 1.2) + 4096;
+    cap1 = (cap1 + 8191) / 8192 * 8192;
     cap2 = (cap2 + 63) / 64 * 64;
     RBX_TRY(c->pc_bits.reserve(ngroups * 16));
-    const uint64_t ncnt = 64 + (uint64_t)nregions;  // cnt1 (padded to 64), cnt2
+    const uint64_t ncnt = 64 * kBkSub + (uint64_t)nregions;  // cnt1 (padded), cnt2
     RBX_TRY(c->pc_cnt.reserve(ncnt * 4));
-    RBX_TRY(c->pc_pairs1.reserve((uint64_t)ncoarse * cap1 * 8));
+    RBX_TRY(c->pc_pairs1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
     RBX_TRY(c->pc_pairs2.reserve((uint64_t)nregions * cap2 * 8));
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
@@ -606,7 +605,7 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
         a.alive = c->pc_bits.as<unsigned long long>();
         a.miss = a.alive + ngroups;
         a.cnt1 = c->pc_cnt.as<uint32_t>();
-        a.cnt2 = a.cnt1 + 64;
+        a.cnt2 = a.cnt1 + 64 * kBkSub;
         a.pairs1 = c->pc_pairs1.as<unsigned long long>();
         a.pairs2 = c->pc_pairs2.as<unsigned long long>();
         a.out = d_out;
@@ -1960,10 +1959,11 @@ int rbx_tune(const char *key, int value) {
         g_partition_mode = value;
         return RBX_OK;
     }
-    // bits 0-1: store variants (results unchanged); bits 2-3: DIAGNOSTICS ONLY, results become
-    // wrong (4: stage 1 emits no pairs; 8: the probe records no misses) -- microbench timing
+    // DIAGNOSTICS ONLY (tools/microbench.py pflags), results become wrong: 4 = stage 1 emits no
+    // pairs, 8 = the probe records no misses.  0 = normal operation.
     if (!strcmp(key, "contains_partition_flags")) {
-        if (value < 0 || value > 15) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in [0, 15]");
+        if (value != 0 && value != 4 && value != 8 && value != 12)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12}");
         g_partition_flags = value;
         return RBX_OK;
     }

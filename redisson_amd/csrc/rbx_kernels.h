@@ -52,6 +52,7 @@ struct AddChunkArgs {
 
 // partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
 constexpr int kBkRegionBits = 19;  // 2^19 bits = 64 KiB bitmap region = one LDS image
+constexpr uint32_t kBkSub = 16;    // sub-partitions (own counters) per coarse bucket
 struct PcArgs {
     KeysDev keys;
     uint64_t base, nchunk;
@@ -62,17 +63,17 @@ struct PcArgs {
     uint32_t fb;            // regions per coarse bucket = 2^fb
     uint32_t cshift;        // kBkRegionBits + fb
     uint32_t ncoarse;       // <= 64
-    uint64_t cap1, cap2;    // pair capacity per coarse bucket / per region
+    uint64_t cap1, cap2;    // pair capacity per coarse sub-partition / per region
     uint64_t nwords4;       // bitmap words rounded up to a multiple of 4
-    uint32_t *cnt1;         // ncoarse, zeroed
+    uint32_t *cnt1;         // ncoarse * kBkSub, zeroed
     uint32_t *cnt2;         // nregions, zeroed
     unsigned long long *alive;  // ceil(nchunk/64)
     unsigned long long *miss;   // ceil(nchunk/64), zeroed
-    unsigned long long *pairs1; // ncoarse * cap1
+    unsigned long long *pairs1; // ncoarse * kBkSub * cap1
     unsigned long long *pairs2; // nregions * cap2
     uint8_t *out;
     unsigned long long *count;
-    uint32_t flags;  // bit 0: plain stores for pair runs; bit 1: 128-byte aligned padded runs
+    uint32_t flags;  // diagnostics only (rbx_tune "contains_partition_flags"); 0 in normal operation
 };
 inline unsigned grid_for_pc(uint64_t n) {
     uint64_t g = ((n + 63) / 64 + 255) / 256;

@@ -382,8 +382,7 @@ def test_full_size_2pow32_property(client, fresh):
     f.delete()
 
 
-@pytest.mark.parametrize("mode", [1, 5, 7])
-def test_partitioned_contains_bucket_overflow(client, fresh, mode):
+def test_partitioned_contains_bucket_overflow(client, fresh):
     """Batches that overflow the partitioned path's fixed bucket capacities (a few keys repeated
     hundreds of thousands of times put all pairs into k-1 buckets): the overflowing pairs are
     probed directly and every per-key answer still equals the oracle's."""
@@ -399,12 +398,10 @@ def test_partitioned_contains_bucket_overflow(client, fresh, mode):
     probe = np.concatenate([base[rng.integers(0, 40, size=400_000)], rng.integers(0, 256, size=(50_000, 32),
                                                                                  dtype=np.uint8)])
     assert L_.lib().rbx_tune(b"contains_partition", 1) == 0
-    assert L_.lib().rbx_tune(b"contains_partition_flags", mode >> 1) == 0
     try:
         cg, pg = f.containsEach(Arena.fixed(probe))
     finally:
         L_.lib().rbx_tune(b"contains_partition", 2)
-        L_.lib().rbx_tune(b"contains_partition_flags", 0)
     cr, pr = ref.contains(*O.fixed_arena(probe), per_key=True)
     assert cg == cr and np.array_equal(pg, pr)
     f.delete()
@@ -523,7 +520,7 @@ def test_mixed_stream_in_order_semantics(client, fresh, seed):
         client.getBloomFilter(n).delete()
 
 
-@pytest.mark.parametrize("mode", [0, 1, 5, 7])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
                                       (14377587, 2, 64), (95850583, 16, 0), (8388608 * 3 + 5, 5, 24)])
 def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
@@ -546,14 +543,12 @@ def test_partitioned_contains_parity(client, fresh, mode, size, k, L):
     ref = O.OracleBloom(size, k)
     f.add(a_add)
     ref.add(*o_add)
-    assert L_.lib().rbx_tune(b"contains_partition", min(mode, 1)) == 0
-    assert L_.lib().rbx_tune(b"contains_partition_flags", mode >> 1) == 0  # 5: plain stores, 7: + aligned runs
+    assert L_.lib().rbx_tune(b"contains_partition", mode) == 0
     try:
         cg, pg = f.containsEach(a_probe)
         c2 = f.contains(a_probe)
     finally:
         L_.lib().rbx_tune(b"contains_partition", 2)
-        L_.lib().rbx_tune(b"contains_partition_flags", 0)
     cr, pr = ref.contains(*o_probe, per_key=True)
     assert cg == cr == c2
     assert np.array_equal(pg, pr)
