@@ -11,9 +11,11 @@ N > 1 is launched by torch.distributed.run, one rank per GPU; C2 does not shard
 ("replicas only"), so every rank runs its own replica with its own keys
 (weak scaling) and `value` = keys of all ranks / max-over-ranks time.
 
-Printed JSON (rank 0, one line) carries `roofline` for the dominant kernel
-(k_bloom_contains) from HIP events on the launch stream, and `cpu_baseline`: the
-oracle's single-thread C restatement timed on a bounded sample on this host.
+Printed JSON (rank 0, one line) carries `roofline` for the contains call -- the partitioned
+pipeline k_bk_stage1 -> k_bk_emit2 -> k_bk_probe -> k_bk_final (contains_partitioned.hip),
+timed with HIP events on the launch stream -- with its PMC traffic and memory-request count
+(profiles/traffic.json, tools/profile_round.sh), an A/B against the direct early-exit kernel,
+and `cpu_baseline`: the oracle's single-thread C restatement timed on a bounded sample.
 """
 from __future__ import annotations
 
@@ -111,11 +113,11 @@ def sum_over_ranks(world, v: int) -> int:
     return int(t.item())
 
 
-def load_traffic(path, kernel):
+def load_traffic(path, kernel, field="hbm_bytes_per_launch"):
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get(kernel, {}).get(field)
     except (OSError, ValueError):
         return None
 
@@ -181,7 +183,7 @@ def run_c2(args, world, rank, local):
     fresh = torch.randint(0, 256, (n - half, 32), dtype=torch.uint8, device="cuda", generator=g)
     probe = torch.cat([added, fresh])
     del fresh
-    cnt = torch.zeros(4, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(4, dtype=torch.int64, device="cuda")  # [0] add, [1] warmup, [2] timed, [3] A/B
 
     # setup: add the first half (timed separately: the "add" half of the metric)
     torch.cuda.synchronize()
@@ -233,12 +235,26 @@ def run_c2(args, world, rank, local):
         assert total_present == present_one * args.steps, "contains count changed between steps"
     assert total_present >= half * args.steps  # no false negatives
 
+    # A/B reference: the same step through the direct early-exit kernel (k_bloom_contains)
+    L.lib().rbx_tune(b"contains_partition", 0)
+    h.contains_dev(dk, cnt.data_ptr() + 24, stream=sptr)
+    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    d0.record(stream)
+    for _ in range(3):
+        h.contains_dev(dk, cnt.data_ptr() + 24, stream=sptr)
+    d1.record(stream)
+    torch.cuda.synchronize()
+    L.lib().rbx_tune(b"contains_partition", 2)
+    direct_ms = d0.elapsed_time(d1) / 3
+    assert int(cnt[3].item()) == 4 * (total_present // args.steps), "direct and partitioned counts differ"
+
     step_s = max_over_ranks(world, max(kern_ms / 1e3, 0.0))
     keys_all = sum_over_ranks(world, n * args.steps)
     value = keys_all / (step_s * args.steps)
     algo_bytes = n * (32 + K * 8)  # 32 B key + k x 8 B gathered per key
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
-    traffic = load_traffic(args.traffic_json, "k_bloom_contains")
+    traffic = load_traffic(args.traffic_json, "contains_pipeline")
+    reqs = load_traffic(args.traffic_json, "contains_pipeline", "requests_per_launch")
     res = {
         "metric": "Bloom contains keys/sec (whole node), C2: one 2^32-bit filter, k=7, 32-byte keys",
         "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -250,13 +266,23 @@ def run_c2(args, world, rank, local):
                    "parallelism": f"replicas x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes_per_launch": algo_bytes, "kernel": "k_bloom_contains<32,8,4>",
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     # one contains call = the partitioned pipeline's kernels in sequence on one stream
+                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<512> + k_bk_probe + k_bk_final",
                      "kernel_avg_ms": kern_ms,
+                     # the binding limit: memory requests at the L2->EA interface (PMC TCC_EA0_RD/WRREQ),
+                     # against the measured random-gather request rate at this working set
+                     "requests_per_launch": reqs,
+                     "request_rate_per_s": (reqs / (kern_ms / 1e3)) if reqs else None,
+                     "request_peak_per_s": gathers_per_s,
+                     "request_frac": (reqs / (kern_ms / 1e3) / gathers_per_s) if reqs else None,
                      # north-star definition: keys/s x k / measured random-gather peak at this
-                     # working set (> 1 is possible: early exit skips gathers of absent keys)
+                     # working set (> 1: early exit and LDS probes avoid most random gathers)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
         "extra": {"add_keys_per_s_per_gpu": half / (add_ms / 1e3), "add_new_keys": n_new,
-                  "present_per_step": total_present // args.steps, "wall_s_timed": wall},
+                  "present_per_step": total_present // args.steps, "wall_s_timed": wall,
+                  "contains_direct_kernel_ms": direct_ms,
+                  "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3)},
     }
     h.close()
     client.shutdown()

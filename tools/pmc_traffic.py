@@ -19,7 +19,9 @@ import json
 import os
 import re
 
-SHORT = [("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains", r"k_bloom_contains<"),
+SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_bk_probe", r"k_bk_probe"),
+         ("k_bk_final", r"k_bk_final"),
+         ("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains", r"k_bloom_contains<"),
          ("k_bloom_add_probe", r"k_bloom_add_probe"), ("k_bloom_add_commit", r"k_bloom_add_commit"),
          ("k_gather_probe", r"k_gather_probe"), ("k_hll_pfadd", r"k_hll_pfadd"), ("k_hll_count", r"k_hll_count"),
          ("k_bitcount", r"k_bitcount")]
@@ -68,7 +70,18 @@ def main():
         if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
             t = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
             e["tcc_hit_rate"] = cs["TCC_HIT_sum"] / t if t else None
+        if "TCC_EA0_RDREQ_sum" in cs and "TCC_EA0_WRREQ_sum" in cs:
+            # memory requests at the L2 -> EA interface (the binding rate for these kernels)
+            e["requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"] + cs["TCC_EA0_WRREQ_sum"]
         out[k] = e
+    # the partitioned contains is one call = these kernels in sequence: sum per call
+    pipe = [k for k in ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_final") if k in out]
+    if pipe:
+        agg = {"kernels": pipe}
+        for f in ("hbm_bytes_per_launch", "requests_per_launch", "fetch_bytes_x2", "write_bytes"):
+            if all(f in out[k] for k in pipe):
+                agg[f] = sum(out[k][f] for k in pipe)
+        out["contains_pipeline"] = agg
     os.makedirs(os.path.dirname(a.o) or ".", exist_ok=True)
     with open(a.o, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)

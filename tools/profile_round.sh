@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profiles the default bench (C2 contains) on one GPU: kernel-trace stats + separate PMC
-# passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) -> gpurun_out/profile_<tag>/.
+# passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss / EA read+write requests) -> gpurun_out/profile_<tag>/.
 # Run through gpurun:  bash tools/profile_round.sh r01 [extra bench args]
 set -u
 TAG=${1:-r01}; shift || true
@@ -14,12 +14,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o p -- python3 $B > "$OUT/pmc_fetch.log" 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o p -- python3 $B > "$OUT/pmc_write.log" 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmc_tcc" -o p -- python3 $B > "$OUT/pmc_tcc.log" 2>&1 || exit 1
-python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" -o "$OUT/traffic.json" > /dev/null || exit 1
+timeout -s KILL 200 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace --output-format csv -d "$OUT/pmc_req" -o p -- python3 $B > "$OUT/pmc_req.log" 2>&1 || exit 1
+python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/pmc_req" -o "$OUT/traffic.json" > /dev/null || exit 1
 # keep summaries only (gpurun copies back <= 64 MiB): stats CSVs, our kernels' counter rows
-for d in pmc_fetch pmc_write pmc_tcc; do
+for d in pmc_fetch pmc_write pmc_tcc pmc_req; do
   f=$(find "$OUT/$d" -name "*counter_collection.csv" | head -1)
   [ -n "$f" ] && { head -1 "$f"; grep -E "rbx::" "$f" | head -200; } > "$OUT/${d}_rbx_rows.csv"
 done
 find "$OUT" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
-rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/trace"
+rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/pmc_req" "$OUT/trace"
 echo "profile $TAG ok"
