@@ -1,0 +1,45 @@
+// bucket_common.h -- helpers shared by the region-partitioned Bloom pipelines
+// (contains_partitioned.hip, add_partitioned.hip): key hashing dispatch and the LDS bucket scan.
+#pragma once
+
+#include "rbx_kernels.h"
+
+namespace rbx {
+
+// HighwayHash128 of key i (Hash.hash128, M/misc/Hash.java:53-74): 16/32/64-byte fast path or
+// the generic any-length path
+template <int KLEN>
+__device__ __forceinline__ void bk_hash(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
+    if constexpr (KLEN > 0) {
+        hh128_fixed<KLEN>(keys.bytes + i * (uint64_t)KLEN, h1, h2);
+    } else {
+        uint64_t a, len;
+        if (keys.offsets) {
+            a = keys.offsets[i];
+            len = keys.offsets[i + 1] - a;
+            a -= keys.off_base;
+        } else {
+            a = i * keys.stride;
+            len = keys.stride;
+        }
+        hh128_bytes(keys.bytes + a, len, h1, h2);
+    }
+}
+
+// exclusive scan of cnt[0..nb) (nb <= 128) by wave 0 into start[] and pos[]
+__device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t a = 2 * lane < nb ? cnt[2 * lane] : 0u;
+    const uint32_t b = 2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u;
+    uint32_t x = a + b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    const uint32_t ex = x - a - b;
+    if (2 * lane < nb) start[2 * lane] = pos[2 * lane] = ex;
+    if (2 * lane + 1 < nb) start[2 * lane + 1] = pos[2 * lane + 1] = ex + a;
+}
+
+}  // namespace rbx

@@ -26,7 +26,7 @@
 // for adversarial batches, e.g. one key repeated 1e8 times) is probed directly from HBM where it
 // overflows, so the answer is exact in every case.  The answer per key is the AND of its k bits,
 // exactly as the direct kernel (bloom_kernels.hip) computes it.
-#include "rbx_kernels.h"
+#include "bucket_common.h"
 
 namespace rbx {
 
@@ -34,24 +34,6 @@ constexpr uint32_t kBkRegionWords = 1u << (kBkRegionBits - 5);  // 16384 words =
 // Each coarse bucket is split into kBkSub sub-partitions with their own reservation counters;
 // stage-1 block b writes to sub-partition b % kBkSub (one counter per bucket would take every
 // block's reservation: ~1e5 same-address atomics per counter per 1e8 keys).
-
-template <int KLEN>
-__device__ __forceinline__ void bk_hash(const KeysDev &keys, uint64_t i, uint64_t &h1, uint64_t &h2) {
-    if constexpr (KLEN > 0) {
-        hh128_fixed<KLEN>(keys.bytes + i * (uint64_t)KLEN, h1, h2);
-    } else {
-        uint64_t a, len;
-        if (keys.offsets) {
-            a = keys.offsets[i];
-            len = keys.offsets[i + 1] - a;
-            a -= keys.off_base;
-        } else {
-            a = i * keys.stride;
-            len = keys.stride;
-        }
-        hh128_bytes(keys.bytes + a, len, h1, h2);
-    }
-}
 
 // a pair whose bucket is full: test its bit in HBM
 __device__ __forceinline__ void bk_direct(unsigned long long e, const uint32_t *__restrict__ bm,
@@ -70,22 +52,6 @@ __device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, ui
         if (gp < cap) __builtin_nontemporal_store(e, dst + gp);
         else bk_direct(e, bm, miss);
     }
-}
-
-// exclusive scan of cnt[0..nb) (nb <= 128) by wave 0 into start[] and pos[]
-__device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t a = 2 * lane < nb ? cnt[2 * lane] : 0u;
-    const uint32_t b = 2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u;
-    uint32_t x = a + b;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if ((int)lane >= off) x += y;
-    }
-    const uint32_t ex = x - a - b;
-    if (2 * lane < nb) start[2 * lane] = pos[2 * lane] = ex;
-    if (2 * lane + 1 < nb) start[2 * lane + 1] = pos[2 * lane + 1] = ex + a;
 }
 
 // K1 -----------------------------------------------------------------------------------

@@ -184,6 +184,7 @@ struct rbx_ctx {
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2;  // partitioned contains
+    DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits;  // partitioned add
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
@@ -497,9 +498,9 @@ static int ensure_table(rbx_ctx *c, uint64_t want_pairs, hipStream_t st) {
     return RBX_OK;
 }
 
-static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, const uint64_t *d_seg_off,
-                   uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
-                   unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
+static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, const uint64_t *d_seg_off,
+                         uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
+                         unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
     if (keys.n == 0) return RBX_OK;
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     const bool narrow = d_filt == nullptr && kmax <= 32;
@@ -543,6 +544,120 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
         HIP_TRY(hipGetLastError());
     }
     return RBX_OK;
+}
+
+// Partitioned add (add_partitioned.hip) for one large filter.  Mode: 0 never, 1 whenever
+// k <= 16, 2 (default) when the bitmap is >= 64 MiB and the batch >= 4M keys.
+static int g_add_partition_mode = 2;
+
+static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
+    if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << kBaRegionBits)) return false;
+    if (g_add_partition_mode == 0) return false;
+    if (g_add_partition_mode == 1) return true;
+    return size >= (1ULL << 29) && n >= (1ULL << 22);
+}
+
+static KeysDev keys_slice(const KeysDev &k, uint64_t i0, uint64_t n) {
+    KeysDev s = k;
+    s.n = n;
+    if (k.offsets) s.offsets = k.offsets + i0;  // offsets stay absolute (off_base unchanged)
+    else s.bytes = k.bytes + i0 * k.stride;
+    return s;
+}
+
+static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out_new,
+                               unsigned long long *d_count, hipStream_t st) {
+    const uint32_t k = f.k;
+    const uint64_t size = f.mp.size;
+    const uint32_t nregions = (uint32_t)((size + (1ULL << kBaRegionBits) - 1) >> kBaRegionBits);
+    uint32_t L = 0;
+    while ((1ULL << L) < nregions) ++L;
+    const uint32_t f3 = std::min<uint32_t>(6, L), f2 = std::min<uint32_t>(6, L - f3);
+    const uint32_t s3 = kBaRegionBits, s2 = s3 + f3, s1 = s2 + f2;
+    const uint32_t ncoarse = (uint32_t)((size + (1ULL << s1) - 1) >> s1);  // <= 64 for size <= 2^32
+    const uint32_t n2 = (uint32_t)((size + (1ULL << s2) - 1) >> s2);
+    // chunk: key ids < 2^26 and the per-region pair capacity fits the LDS record image
+    const double per_region = (double)k * (double)(1ULL << kBaRegionBits) / (double)size;  // pairs per key
+    uint64_t chunk = (uint64_t)((kBaMaxRegionPairs - 512) / 1.3 / per_region);
+    chunk = std::min<uint64_t>(chunk, 1ULL << 26);
+    const uint64_t nch = (keys.n + chunk - 1) / chunk;
+    chunk = (keys.n + nch - 1) / nch;
+    const double pairs = (double)chunk * k;
+    auto cap_of = [&](uint32_t shift, double slack, uint64_t add, uint64_t round) {
+        const double frac = std::min(1.0, (double)(1ULL << shift) / (double)size);
+        uint64_t cap = (uint64_t)(pairs * frac * slack) + add;
+        return (cap + round - 1) / round * round;
+    };
+    const uint64_t cap1 = cap_of(s1, 1.15 / kBkSub, 8192, 8192);
+    const uint64_t cap2 = cap_of(s2, 1.15, 8192, 8192);
+    const uint64_t cap3 = std::min<uint64_t>(kBaMaxRegionPairs, cap_of(s3, 1.3, 256, 64));
+    const uint32_t nranges = (uint32_t)((chunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
+    const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;
+    const uint64_t b1 = (uint64_t)ncoarse * kBkSub * cap1 * 8, b3 = (uint64_t)nregions * cap3 * 8;
+    RBX_TRY(c->pa_p1.reserve(std::max(b1, b3)));  // level 3 reuses level 1's buffer (consumed by level 2)
+    RBX_TRY(c->pa_p2.reserve((uint64_t)n2 * cap2 * 8));
+    const uint64_t ncnt = 64 * kBkSub + n2 + nregions + nranges + 1;
+    RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
+    RBX_TRY(c->pa_recs.reserve((uint64_t)nranges * cap_rec * 4));
+    const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);
+    RBX_TRY(c->pa_bits.reserve(nbw * 4));
+    const int fl = fast_len(keys);
+    for (uint64_t base = 0; base < keys.n; base += chunk) {
+        BaArgs a{};
+        a.keys = keys;
+        a.base = base;
+        a.nchunk = std::min<uint64_t>(chunk, keys.n - base);
+        a.f = f;
+        a.ncoarse = ncoarse;
+        a.s1 = s1;
+        a.s2 = s2;
+        a.s3 = s3;
+        a.f2 = f2;
+        a.f3 = f3;
+        a.n2 = n2;
+        a.nregions = nregions;
+        a.cap1 = cap1;
+        a.cap2 = cap2;
+        a.cap3 = cap3;
+        a.cap_rec = cap_rec;
+        a.p1 = c->pa_p1.as<unsigned long long>();
+        a.p2 = c->pa_p2.as<unsigned long long>();
+        a.p3 = a.p1;
+        a.cnt1 = c->pa_cnt.as<uint32_t>();
+        a.cnt2 = a.cnt1 + 64 * kBkSub;
+        a.cnt3 = a.cnt2 + n2;
+        a.rec_cnt = a.cnt3 + nregions;
+        a.overflow = a.rec_cnt + nranges;
+        a.recs = c->pa_recs.as<uint32_t>();
+        a.nranges = (uint32_t)((a.nchunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
+        a.new_bits = c->pa_bits.as<uint32_t>();
+        a.nwords4 = (size + 127) / 128 * 4;
+        a.out_new = d_out_new;
+        a.count = d_count;
+        HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
+        HIP_TRY(hipMemsetAsync(a.new_bits, 0, ((uint64_t)a.nranges << (kBaKeyRangeBits - 5)) * 4, st));
+        launch_add_partitioned_chunk(a, fl, st);
+        HIP_TRY(hipGetLastError());
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, a.overflow, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (ovf) {
+            // a bucket overflowed before any bitmap word changed: this chunk on the table path
+            const KeysDev sub = keys_slice(keys, base, a.nchunk);
+            RBX_TRY(run_add_table(c, sub, nullptr, nullptr, 0, f, k, d_out_new ? d_out_new + base : nullptr, d_count,
+                                  nullptr, st));
+        }
+    }
+    return RBX_OK;
+}
+
+static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, const uint64_t *d_seg_off,
+                   uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
+                   unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
+    if (keys.n == 0) return RBX_OK;
+    if (d_filt == nullptr && use_add_partitioned(single.mp.size, single.k, keys.n))
+        return run_add_partitioned(c, keys, single, d_out_new, d_count, st);
+    return run_add_table(c, keys, d_filt, d_seg_off, nseg, single, kmax, d_out_new, d_count, d_seg_counts, st);
 }
 
 // Partitioned contains (contains_partitioned.hip) for one large filter.  Mode: 0 never,
@@ -1965,6 +2080,11 @@ int rbx_tune(const char *key, int value) {
         if (value != 0 && value != 4 && value != 8 && value != 12)
             return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12}");
         g_partition_flags = value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_partition")) {
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition in [0, 2]");
+        g_add_partition_mode = value;
         return RBX_OK;
     }
     if (!strcmp(key, "contains_stage1")) {

@@ -81,6 +81,31 @@ inline unsigned grid_for_pc(uint64_t n) {
 }
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
 
+// partitioned single-filter add (add_partitioned.hip): one chunk of keys
+constexpr int kBaRegionBits = 15;               // 32K-bit regions: owner array (128 KiB) + bitmap (4 KiB) in LDS
+constexpr int kBaKeyRangeBits = 20;             // records bucketed by 2^20-key ranges (128 KiB LDS bitmap)
+constexpr uint32_t kBaMaxRegionPairs = 6144;    // LDS record image: cap3 <= this
+struct BaArgs {
+    KeysDev keys;
+    uint64_t base, nchunk;
+    FilterDesc f;                 // bm, redis_len, mp, k
+    uint32_t ncoarse;             // level-1 buckets (each kBkSub sub-partitions)
+    uint32_t s1, s2, s3;          // partition id = idx >> s at levels 1, 2, 3 (s3 = kBaRegionBits)
+    uint32_t f2, f3;              // fan-out bits of levels 2 and 3
+    uint32_t n2, nregions;        // level-2 partitions, regions
+    uint64_t cap1, cap2, cap3, cap_rec;
+    unsigned long long *p1, *p2, *p3;  // pair arrays (p3 may alias p1)
+    uint32_t *cnt1, *cnt2, *cnt3, *rec_cnt;  // zeroed per chunk
+    uint32_t *recs;               // nranges x cap_rec owner key ids
+    uint32_t nranges;
+    uint32_t *new_bits;           // nranges x 2^15 words, zeroed per chunk
+    uint32_t *overflow;           // zeroed; set when a pair does not fit (the chunk then reruns on the table path)
+    uint64_t nwords4;             // bitmap words rounded up to a multiple of 4
+    uint8_t *out_new;
+    unsigned long long *count;
+};
+void launch_add_partitioned_chunk(const BaArgs &a, int klen_fast, hipStream_t st);
+
 // ordered mixed contains/add stream (one chunk of keys)
 struct StreamChunkArgs {
     KeysDev keys;

@@ -609,3 +609,64 @@ def test_pinned_host_arena(client, fresh):
         f.delete()
     finally:
         L_.lib().rbx_host_free(p)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
+                                      ((1 << 29) + 3, 16, 0), (1 << 20, 3, 24), (100_003, 2, 64)])
+def test_partitioned_add_parity(client, fresh, mode, size, k, L):
+    """add() through the LDS-region partitioned pipeline (mode 1, forced) and the first-setter table
+    (mode 0): per-key new flags, the count, the Redis bitmap bytes and length equal the oracle's
+    in-order SETBIT fold, for a second batch that repeats keys within itself and re-adds keys of
+    the first batch."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(size % 997 + 31 * k + L)
+    n = 200_000
+    if L:
+        mat = rng.integers(0, 256, size=(n, L), dtype=np.uint8)
+        first = mat[: n // 4]
+        second = np.concatenate([mat[n // 8: n // 2], mat[rng.integers(0, n // 2, size=n // 4)], mat[n // 2:]])
+        arenas = [(Arena.fixed(first), O.fixed_arena(first)), (Arena.fixed(second), O.fixed_arena(second))]
+    else:
+        keys = [rng.bytes(int(x)) for x in rng.integers(0, 90, size=n)]
+        first = keys[: n // 4]
+        second = keys[n // 8: n // 2] + [keys[i] for i in rng.integers(0, n // 2, size=n // 4)] + keys[n // 2:]
+        arenas = [(Arena(first), O.arena(first)), (Arena(second), O.arena(second))]
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(size, k)
+    ref = O.OracleBloom(size, k)
+    assert L_.lib().rbx_tune(b"add_partition", mode) == 0
+    try:
+        for a, o in arenas:
+            cg, ng = f.addEach(a)
+            cr, nr = ref.add(*o, per_key=True)
+            assert cg == cr and np.array_equal(ng, nr)
+    finally:
+        L_.lib().rbx_tune(b"add_partition", 2)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.count() == ref.count()
+    f.delete()
+
+
+def test_partitioned_add_overflow_falls_back(client, fresh):
+    """A batch that overflows the partitioned add's bucket capacities (40 keys repeated 400k
+    times) reruns on the first-setter table: flags, count and bitmap still equal the oracle's."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, size=(40, 32), dtype=np.uint8)
+    batch = np.concatenate([base[rng.integers(0, 40, size=400_000)], rng.integers(0, 256, size=(30_000, 32),
+                                                                                 dtype=np.uint8)])
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 30, 7)
+    ref = O.OracleBloom(1 << 30, 7)
+    assert L_.lib().rbx_tune(b"add_partition", 1) == 0
+    try:
+        cg, ng = f.addEach(Arena.fixed(batch))
+    finally:
+        L_.lib().rbx_tune(b"add_partition", 2)
+    cr, nr = ref.add(*O.fixed_arena(batch), per_key=True)
+    assert cg == cr and np.array_equal(ng, nr)
+    assert f.exportBitmap() == ref.redis_string()
+    f.delete()

@@ -142,6 +142,43 @@ def main():
         h.close()
         fb.delete()
 
+    if "pa2" in a.what:
+        # one default-path add of n/2 keys into an empty 2^32-bit filter (short run for PMC passes)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        fb = client.getBloomFilter("pa2")
+        fb.tryInitRaw(1 << 32, 7)
+        h = BloomHandle(client, "pa2")
+        ms = timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), n // 2, 32), cnt.data_ptr(), stream=sp), 1)
+        print(json.dumps({"bench": "pa2", "ms": ms, "keys_per_s": n // 2 / (ms / 1e3), "new": int(cnt[0].item())}))
+        h.close()
+        fb.delete()
+
+    if "padd" in a.what:
+        # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        for name, size, k in [("C2_2^32", 1 << 32, 7), ("C2_twin", 4294967293, 7)]:
+            res = {0: [], 1: []}
+            news = {}
+            for rnd in range(3):
+                for mode in res:
+                    L.lib().rbx_tune(b"add_partition", mode)
+                    fb = client.getBloomFilter(f"pa-{name}-{rnd}-{mode}")
+                    fb.tryInitRaw(size, k)
+                    h = BloomHandle(client, f"pa-{name}-{rnd}-{mode}")
+                    cnt.zero_()
+                    res[mode].append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32),
+                                                                     cnt.data_ptr(), stream=sp), 1))
+                    news[mode] = int(cnt[0].item())
+                    h.close()
+                    fb.delete()
+            assert news[0] == news[1], news
+            for mode, v in res.items():
+                med = statistics.median(v)
+                print(json.dumps({"bench": "add_partition", "filter": name, "mode": mode, "keys": m, "ms_median": med,
+                                  "keys_per_s": m / (med / 1e3), "new": news[mode]}), flush=True)
+        L.lib().rbx_tune(b"add_partition", 2)
+
     if "pflags" in a.what:
         # direct vs partitioned contains, and the partitioned path with its diagnostic switches
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
