@@ -206,6 +206,25 @@ struct rbx_ctx {
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf slot_bytes[2], slot_offs[2];
     uint64_t staging_bytes = 64ull << 20;
+
+    // stream order of the scratch above across calls issued on different streams (ScratchOrder)
+    hipEvent_t ev_scratch = nullptr;
+    hipStream_t scratch_stream = nullptr;
+};
+
+// Every call that enqueues work touching the context's scratch (first-setter table, pair
+// buckets, staging, descriptor tables, counters) runs on the device after the previous such
+// call, also when the two were issued on different streams: the new stream waits on an event
+// the previous user recorded.  (The host mutex orders the calls; this orders their kernels.)
+struct ScratchOrder {
+    rbx_ctx *c;
+    hipStream_t st;
+    ScratchOrder(rbx_ctx *c_, hipStream_t st_) : c(c_), st(st_) {
+        if (c->ev_scratch && c->scratch_stream && c->scratch_stream != st) (void)hipStreamWaitEvent(st, c->ev_scratch, 0);
+    }
+    ~ScratchOrder() {
+        if (c->ev_scratch && hipEventRecord(c->ev_scratch, st) == hipSuccess) c->scratch_stream = st;
+    }
 };
 
 static constexpr size_t kHllBytes = 16384;
@@ -783,6 +802,7 @@ int rbx_init(int device, rbx_ctx **out) {
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming);
+        if (e == hipSuccess && i == 0) e = hipEventCreateWithFlags(&c->ev_scratch, hipEventDisableTiming);
     }
     if (e != hipSuccess) {
         delete c;
@@ -807,6 +827,7 @@ int rbx_shutdown(rbx_ctx *c) {
     for (int i = 0; i < 2; ++i) {
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
         if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
+        if (i == 0 && c->ev_scratch) (void)hipEventDestroy(c->ev_scratch);
     }
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1012,6 +1033,7 @@ static int bloom_host_op(rbx_ctx *c, const char *name, uint64_t size, uint32_t k
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "ctx/name is NULL");
     RBX_TRY(validate_keys(keys));
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     // add()/contains() first read the config if the caller has none cached (:106-108)
     if (size == 0) {
@@ -1084,6 +1106,7 @@ static int bitcount_locked(rbx_ctx *c, const std::string &name, uint64_t *out) {
 int rbx_bloom_bitcount(rbx_ctx *c, const char *name, uint64_t *out) {
     if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     return bitcount_locked(c, name, out);
 }
@@ -1092,6 +1115,7 @@ int rbx_bloom_bitcount(rbx_ctx *c, const char *name, uint64_t *out) {
 int rbx_bloom_count(rbx_ctx *c, const char *name, int64_t *out) {
     if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     BloomConfig *cfg;
     RBX_TRY(get_config(c, name, &cfg));
@@ -1167,6 +1191,7 @@ int rbx_bloom_renamenx(rbx_ctx *c, const char *name, const char *new_name, int *
 int rbx_bloom_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *redis_len) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     Entry *e = find(c, name);
     if (!e) {
@@ -1190,6 +1215,7 @@ int rbx_bloom_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_
     if (!c || !name || (len && !bytes)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     if (len > (1ULL << 29)) return fail(RBX_E_ILLEGAL_ARGUMENT, "string exceeds the 512 MiB Redis limit");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::shared_ptr<Bitmap> b;
     uint64_t bits = len * 8;
@@ -1209,6 +1235,7 @@ int rbx_bloom_import_dev(rbx_ctx *c, const char *name, const uint8_t *d_bytes, u
     if (!c || !name || (len && !d_bytes)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     if (len > (1ULL << 29)) return fail(RBX_E_ILLEGAL_ARGUMENT, "string exceeds the 512 MiB Redis limit");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     hipStream_t st = pick_stream(c, stream);
     uint64_t bits = len * 8;
@@ -1268,6 +1295,7 @@ int rbx_bloom_contains_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uin
     RBX_TRY(validate_keys(d_keys));
     if (d_keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     KeysDev k = keys_dev(d_keys);
     FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
@@ -1280,6 +1308,7 @@ int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t 
     RBX_TRY(validate_keys(d_keys));
     if (d_keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     KeysDev k = keys_dev(d_keys);
     FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
@@ -1320,6 +1349,7 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     if (!c || !filters || !d_seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
     RBX_TRY(validate_keys(d_keys));
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
@@ -1340,6 +1370,7 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     if (!c || !filters || !d_seg_offsets || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
     RBX_TRY(validate_keys(d_keys));
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
@@ -1361,6 +1392,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
         return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
     RBX_TRY(validate_keys(d_keys));
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
@@ -1402,6 +1434,7 @@ int rbx_bloom_stream(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, c
     for (uint64_t i = 0; i < keys->n; ++i)
         if (key_filter[i] >= nfilters) return fail(RBX_E_ILLEGAL_ARGUMENT, "key_filter index out of range");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     KeysDev dk;
     RBX_TRY(upload_keys(c, keys, 0, keys->n, &dk));
@@ -1445,6 +1478,7 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
         if (seg_offsets[s + 1] == seg_offsets[s]) return fail(RBX_E_ARITHMETIC, "/ by zero");
     }
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     KeysDev dk;
     RBX_TRY(upload_keys(c, keys, 0, keys->n, &dk));
@@ -1555,6 +1589,7 @@ int rbx_hll_add_multi(rbx_ctx *c, const char *const *names, uint32_t nseg, const
     for (uint32_t s = 0; s < nseg; ++s)
         if (seg_offsets[s + 1] < seg_offsets[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must be ascending");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<HllState *> hl(nseg);
     std::vector<std::shared_ptr<HllState>> keep(nseg);
@@ -1700,6 +1735,7 @@ static int pfcount_each(rbx_ctx *c, const std::vector<HllState *> &hl, uint64_t 
 int rbx_hll_count_each(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *out) {
     if (!c || (n && (!names || !out))) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<HllState *> hl(n);
     std::vector<std::shared_ptr<HllState>> keep(n);
@@ -1714,6 +1750,7 @@ int rbx_hll_count(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *ou
     if (!c || !names || !out || n == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
     if (n == 1) return rbx_hll_count_each(c, names, 1, out);
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<std::shared_ptr<HllState>> keep;
     std::vector<uint8_t *> srcs;
@@ -1742,6 +1779,7 @@ int rbx_hll_count(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *ou
 int rbx_hll_merge(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_t nsrc) {
     if (!c || !dest || (nsrc && !srcs)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<std::shared_ptr<HllState>> keep;
     std::vector<uint8_t *> sp;
@@ -1770,6 +1808,7 @@ int rbx_hll_merge(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_
 int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *len) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::shared_ptr<HllState> h;
     RBX_TRY(hll_get(c, name, false, &h, nullptr));
@@ -1837,6 +1876,7 @@ int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t 
         if (idx != 16384) return fail(RBX_E_WRONGTYPE, bad);
     }
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     auto it = c->ks.find(name);
     std::shared_ptr<HllState> h;
@@ -1904,6 +1944,7 @@ int rbx_hll_add_multi_dev(rbx_ctx *c, rbx_hll *const *hlls, uint32_t nseg, const
     if (!c || !hlls || !h_seg_offsets || !d_changed) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     RBX_TRY(validate_keys(d_elements));
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
     std::vector<HllState *> hl(nseg);
     for (uint32_t s = 0; s < nseg; ++s) {
@@ -1917,6 +1958,7 @@ int rbx_hll_add_multi_dev(rbx_ctx *c, rbx_hll *const *hlls, uint32_t nseg, const
 int rbx_hll_count_each_handles(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n, uint64_t *out) {
     if (!c || (n && (!hlls || !out))) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<HllState *> hl(n);
     for (uint32_t i = 0; i < n; ++i) hl[i] = hlls[i] ? hlls[i]->st.get() : nullptr;
@@ -1949,6 +1991,7 @@ int rbx_rccl_init(rbx_ctx *c, const uint8_t id[128], int nranks, int rank) {
 int rbx_hll_allreduce_max(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n) {
     if (!c || (n && !hlls)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    ScratchOrder so_(c, c->stream);
     if (!c->comm) return fail(RBX_E_ILLEGAL_STATE, "rbx_rccl_init has not been called");
     RBX_TRY(set_device(c));
     // coalesce runs of adjacent register blocks into one all-reduce each

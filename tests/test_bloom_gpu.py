@@ -670,3 +670,36 @@ def test_partitioned_add_overflow_falls_back(client, fresh):
     assert cg == cr and np.array_equal(ng, nr)
     assert f.exportBitmap() == ref.redis_string()
     f.delete()
+
+
+def test_cross_stream_calls_run_in_call_order(client, fresh):
+    """Device-path calls issued on different streams run in call order (the context's scratch and
+    the bitmap are ordered by an event chain): add on stream A, then contains of the same keys on
+    stream B sees every key, and a second add on B sees none as new; partitioned and table paths."""
+    import torch
+
+    from redisson_amd import device_keys
+
+    n = 4_300_000  # above the partitioned paths' 2^22-key threshold
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for size in (1 << 32, 95850583):
+        name = f"{fresh}-{size}"
+        f = client.getBloomFilter(name)
+        f.tryInitRaw(size, 7)
+        h = BloomHandle(client, name)
+        cnt = torch.zeros(4, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        dk = device_keys(keys.data_ptr(), n, 32)
+        h.add_dev(dk, cnt.data_ptr(), stream=sa.cuda_stream)
+        h.contains_dev(dk, cnt.data_ptr() + 8, stream=sb.cuda_stream)
+        h.add_dev(dk, cnt.data_ptr() + 16, stream=sb.cuda_stream)
+        h.contains_dev(dk, cnt.data_ptr() + 24, stream=sa.cuda_stream)
+        torch.cuda.synchronize()
+        c = cnt.tolist()
+        assert c[1] == n and c[2] == 0 and c[3] == n, (size, c)
+        assert c[0] >= n * 0.999  # in-batch false positives of the smaller filter (~1e-4 at its end fill)
+        h.close()
+        f.delete()
