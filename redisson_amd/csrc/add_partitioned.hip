@@ -198,7 +198,7 @@ __global__ __launch_bounds__(1024) void k_ba_region(const unsigned long long *__
                                                     uint32_t *__restrict__ bm, uint64_t nwords4,
                                                     uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt,
                                                     uint64_t cap_rec, uint32_t nranges,
-                                                    const uint32_t *__restrict__ overflow) {
+                                                    const uint32_t *__restrict__ overflow, uint32_t diag) {
     constexpr uint32_t NT = 1024, PER = kBaMaxRegionPairs / NT;
     __shared__ uint32_t s_owner[1u << kBaRegionBits];  // 128 KiB
     __shared__ uint32_t s_bm[kBaRegionWords];          // 4 KiB
@@ -261,6 +261,11 @@ __global__ __launch_bounds__(1024) void k_ba_region(const unsigned long long *__
         }
         const bool dirty = __syncthreads_or(any);
         if (!dirty) continue;  // uniform: nothing owned (every touched bit was already 1)
+        if (diag & 4) {        // diagnostics: bitmap write-back only, no records
+            if (threadIdx.x < nw) bm[w0 + threadIdx.x] = s_bm[threadIdx.x];
+            __syncthreads();
+            continue;
+        }
         uint32_t gb = 0;
         const uint32_t qown = threadIdx.x - 128;
         const bool reserver = threadIdx.x >= 128 && qown < nranges;
@@ -277,7 +282,8 @@ __global__ __launch_bounds__(1024) void k_ba_region(const unsigned long long *__
         }
         if (reserver) s_rgb[qown] = gb;  // the reservation's round trip overlapped the placement
         __syncthreads();
-        // records per range <= 2^20 keys x k: cap_rec bounds them exactly, no overflow
+        // records per range <= 2^20 keys x k: cap_rec bounds them exactly, no overflow.  (Splitting
+        // the range counters 16 ways by block, as stage A does, measured no faster here.)
         for (uint32_t q = wave; q < nranges; q += NT / 64) {
             const uint32_t rn = s_rc[q], st = s_rstart[q];
             uint32_t *dst = recs + (uint64_t)q * cap_rec + s_rgb[q];
@@ -373,7 +379,7 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(512), 0, st, a.p2, a.cnt2, a.cap2, a.n2, 1u, it2, a.s3, a.f3,
                        a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
     hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, 4096)), dim3(1024), 0, st, a.p3, a.cnt3, a.cap3,
-                       a.nregions, a.f.bm, a.nwords4, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow);
+                       a.nregions, a.f.bm, a.nwords4, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow, a.diag);
     hipLaunchKernelGGL(k_ba_keys, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow);
     hipLaunchKernelGGL(k_ba_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.new_bits, a.nchunk, a.base,

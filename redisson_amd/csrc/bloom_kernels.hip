@@ -222,28 +222,28 @@ __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, cons
                                                               const uint32_t *__restrict__ tile_seg0,
                                                               uint8_t *__restrict__ out,
                                                               unsigned long long *__restrict__ counts) {
-    __shared__ uint64_t s_off[257];
+    // No LDS staging and no block barrier: each lane finds its segment by a binary search of
+    // seg_off between the segments of its own and the next 256-key tile (L2-resident; 0-1 steps
+    // for C3-sized segments), so waves run independently and a lane's early-exit depth never
+    // holds up the other waves of its block.
     const uint64_t nkeys = keys.n;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < nkeys; b0 += (uint64_t)gridDim.x * 256) {
-        const uint32_t s0 = tile_seg0[b0 >> 8];
-        for (uint32_t t = threadIdx.x; t < 257; t += blockDim.x) {
-            const uint32_t s = s0 + t;
-            s_off[t] = s <= nseg ? seg_off[s] : ~0ULL;
-        }
-        __syncthreads();
-        const uint64_t i = b0 + threadIdx.x;
+    const uint64_t ntiles = (nkeys + 255) >> 8;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // grid-stride over whole waves: every lane of a wave takes the same trip count
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i - (threadIdx.x & 63) < nkeys; i += stride) {
         const bool active = i < nkeys;
         uint32_t seg = 0;
         bool p = false;
         if (active) {
-            uint32_t lo = 0, hi = 257;  // s_off[lo] <= i < s_off[hi]
+            const uint64_t t = i >> 8;
+            uint32_t lo = tile_seg0[t];                                   // seg_off[lo] <= i
+            uint32_t hi = t + 1 < ntiles ? tile_seg0[t + 1] + 1 : nseg;  // i < seg_off[hi]
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (s_off[mid] <= i) lo = mid;
+                if (seg_off[mid] <= i) lo = mid;
                 else hi = mid;
             }
-            // lo == 256: more than 256 (empty) segments start inside this block
-            seg = lo < 256 ? s0 + lo : upper_seg(seg_off, nseg, i);
+            seg = lo;
             const FilterDesc f = filt[seg];
             uint64_t h1, h2;
             hash_key<KLEN>(keys, i, h1, h2);
@@ -251,7 +251,6 @@ __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, cons
             if (out) out[i] = p;
         }
         if (counts) wave_seg_add(active, seg, p, counts);
-        __syncthreads();
     }
 }
 

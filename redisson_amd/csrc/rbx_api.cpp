@@ -568,6 +568,7 @@ static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_fi
 // Partitioned add (add_partitioned.hip) for one large filter.  Mode: 0 never, 1 whenever
 // k <= 16, 2 (default) when the bitmap is >= 64 MiB and the batch >= 4M keys.
 static int g_add_partition_mode = 2;
+static int g_add_partition_diag = 0;
 
 static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << kBaRegionBits)) return false;
@@ -611,7 +612,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     const uint64_t cap2 = cap_of(s2, 1.15, 8192, 8192);
     const uint64_t cap3 = std::min<uint64_t>(kBaMaxRegionPairs, cap_of(s3, 1.3, 256, 64));
     const uint32_t nranges = (uint32_t)((chunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
-    const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;
+    const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;  // records per key range <= 2^20 keys x k
     const uint64_t b1 = (uint64_t)ncoarse * kBkSub * cap1 * 8, b3 = (uint64_t)nregions * cap3 * 8;
     RBX_TRY(c->pa_p1.reserve(std::max(b1, b3)));  // level 3 reuses level 1's buffer (consumed by level 2)
     RBX_TRY(c->pa_p2.reserve((uint64_t)n2 * cap2 * 8));
@@ -653,6 +654,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.nwords4 = (size + 127) / 128 * 4;
         a.out_new = d_out_new;
         a.count = d_count;
+        a.diag = (uint32_t)g_add_partition_diag;
         HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
         HIP_TRY(hipMemsetAsync(a.new_bits, 0, ((uint64_t)a.nranges << (kBaKeyRangeBits - 5)) * 4, st));
         launch_add_partitioned_chunk(a, fl, st);
@@ -2123,6 +2125,13 @@ int rbx_tune(const char *key, int value) {
         if (value != 0 && value != 4 && value != 8 && value != 12)
             return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12}");
         g_partition_flags = value;
+        return RBX_OK;
+    }
+    // DIAGNOSTICS ONLY (tools/microbench.py padiag), results become wrong: 4 = the region kernel
+    // emits no records.  0 = normal.
+    if (!strcmp(key, "add_partition_diag")) {
+        if (value != 0 && value != 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag in {0, 4}");
+        g_add_partition_diag = value;
         return RBX_OK;
     }
     if (!strcmp(key, "add_partition")) {

@@ -103,6 +103,7 @@ struct BaArgs {
     uint64_t nwords4;             // bitmap words rounded up to a multiple of 4
     uint8_t *out_new;
     unsigned long long *count;
+    uint32_t diag;                // diagnostics only (rbx_tune "add_partition_diag"); 0 in normal operation
 };
 void launch_add_partitioned_chunk(const BaArgs &a, int klen_fast, hipStream_t st);
 

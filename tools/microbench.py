@@ -153,6 +153,25 @@ def main():
         h.close()
         fb.delete()
 
+    if "padiag" in a.what:
+        # partitioned add with its diagnostic switches (wrong results, timing only)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        res = {0: [], 4: []}
+        for rnd in range(3):
+            for dg in res:
+                L.lib().rbx_tune(b"add_partition_diag", dg)
+                fb = client.getBloomFilter(f"pd-{rnd}-{dg}")
+                fb.tryInitRaw(1 << 32, 7)
+                h = BloomHandle(client, f"pd-{rnd}-{dg}")
+                res[dg].append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(),
+                                                               stream=sp), 1))
+                h.close()
+                fb.delete()
+        L.lib().rbx_tune(b"add_partition_diag", 0)
+        for dg, v in res.items():
+            print(json.dumps({"bench": "add_partition_diag", "diag": dg, "ms_median": statistics.median(v)}), flush=True)
+
     if "padd" in a.what:
         # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
