@@ -566,7 +566,8 @@ static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_fi
 }
 
 // Partitioned add (add_partitioned.hip) for one large filter.  Mode: 0 never, 1 whenever
-// k <= 16, 2 (default) when the bitmap is >= 64 MiB and the batch >= 4M keys.
+// k <= 16, 2 (default) when the bitmap is >= 8 MiB and the batch >= 1M keys (measured faster than
+// the first-setter table at every size from 8 MiB to 512 MiB: tools/microbench.py psizes).
 static int g_add_partition_mode = 2;
 static int g_add_partition_diag = 0;
 
@@ -574,7 +575,7 @@ static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << kBaRegionBits)) return false;
     if (g_add_partition_mode == 0) return false;
     if (g_add_partition_mode == 1) return true;
-    return size >= (1ULL << 29) && n >= (1ULL << 22);
+    return size >= (1ULL << 26) && n >= (1ULL << 20);
 }
 
 static KeysDev keys_slice(const KeysDev &k, uint64_t i0, uint64_t n) {
@@ -682,8 +683,9 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
 }
 
 // Partitioned contains (contains_partitioned.hip) for one large filter.  Mode: 0 never,
-// 1 whenever k in [2, 16], 2 (default) when the bitmap is >= 64 MiB and the batch >= 4M keys:
-// there the random-gather rate binds the direct kernel (DESIGN.md §3.6 has the measurements).
+// 1 whenever k in [2, 16], 2 (default) when the bitmap is >= 256 MiB and the batch >= 4M keys.
+// Below 256 MiB the direct kernel measured faster (its early exit costs ~1 gather per absent
+// key, and smaller bitmaps gather partly from L2/MALL); DESIGN.md §3.6 has the size sweep.
 static int g_partition_mode = 2;
 static int g_partition_flags = 0;
 
@@ -691,7 +693,7 @@ static bool use_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 2 || k > 16 || size > (1ULL << 32)) return false;
     if (g_partition_mode == 0) return false;
     if (g_partition_mode == 1) return true;
-    return size >= (1ULL << 29) && n >= (1ULL << 22);
+    return size >= (1ULL << 31) && n >= (1ULL << 22);
 }
 
 static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,

@@ -142,6 +142,36 @@ def main():
         h.close()
         fb.delete()
 
+    if "psizes" in a.what:
+        # direct vs partitioned contains and add over filter sizes, at C2's fill (86 bits per added key)
+        cnt = torch.zeros(4, dtype=torch.int64, device="cuda")
+        for lg in [26, 27, 28, 29, 30, 31, 32]:
+            size = 1 << lg
+            n_add = min(n // 2, size // 86)
+            res = {}
+            for mode in (0, 1):
+                L.lib().rbx_tune(b"add_partition", mode)
+                L.lib().rbx_tune(b"contains_partition", mode)
+                fb = client.getBloomFilter(f"ps-{lg}-{mode}")
+                fb.tryInitRaw(size, 7)
+                h = BloomHandle(client, f"ps-{lg}-{mode}")
+                cnt.zero_()
+                add_ms = timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), n_add, 32), cnt.data_ptr(),
+                                                         stream=sp), 1)
+                dk = device_keys(keys.data_ptr(), n, 32)
+                h.contains_dev(dk, cnt.data_ptr() + 8, stream=sp)
+                c_ms = statistics.median([timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 16, stream=sp), 2)
+                                          for _ in range(3)])
+                res[mode] = (add_ms, c_ms, int(cnt[0].item()), int(cnt[1].item()))
+                h.close()
+                fb.delete()
+            assert res[0][2:] == res[1][2:], res
+            print(json.dumps({"bench": "psizes", "size_log2": lg, "added": n_add,
+                              "add_ms_direct": res[0][0], "add_ms_part": res[1][0],
+                              "contains_ms_direct": res[0][1], "contains_ms_part": res[1][1]}), flush=True)
+        L.lib().rbx_tune(b"add_partition", 2)
+        L.lib().rbx_tune(b"contains_partition", 2)
+
     if "pa2" in a.what:
         # one default-path add of n/2 keys into an empty 2^32-bit filter (short run for PMC passes)
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
