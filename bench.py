@@ -122,6 +122,35 @@ def load_traffic(path, kernel, field="hbm_bytes_per_launch"):
         return None
 
 
+def gather_peak(client, nbytes, nkeys, k, stream, gen):
+    """Random 4-byte gathers/s over an nbytes table (k per key, nkeys keys): the request-rate
+    roofline the Bloom kernels are measured against (k_gather_probe, same MLP structure)."""
+    import torch
+
+    from redisson_amd import _lib as L
+
+    sptr = stream.cuda_stream
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    table = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    table.random_(0, 255, generator=gen)
+    L.lib().rbx_bench_gather(client.ctx, table.data_ptr(), nbytes, nkeys, k, sink.data_ptr(), sptr)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(3):
+        L.lib().rbx_bench_gather(client.ctx, table.data_ptr(), nbytes, nkeys, k, sink.data_ptr(), sptr)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del table
+    return nkeys * k / (e0.elapsed_time(e1) / 3 / 1e3)
+
+
+def request_fields(traffic_json, kernel, ms, peak):
+    """PMC memory requests per launch (TCC_EA0_RDREQ + WRREQ, profiles/traffic.json) vs the peak."""
+    reqs = load_traffic(traffic_json, kernel, "requests_per_launch")
+    return {"requests_per_launch": reqs, "request_rate_per_s": reqs / (ms / 1e3) if reqs else None,
+            "request_peak_per_s": peak, "request_frac": reqs / (ms / 1e3) / peak if reqs and peak else None}
+
+
 # ------------------------------------------------------------------------------------------
 # CPU baseline: oracle restatement (single thread) on a bounded sample of the same workload
 # ------------------------------------------------------------------------------------------
@@ -282,7 +311,11 @@ def run_c2(args, world, rank, local):
         "extra": {"add_keys_per_s_per_gpu": half / (add_ms / 1e3), "add_new_keys": n_new,
                   "present_per_step": total_present // args.steps, "wall_s_timed": wall,
                   "contains_direct_kernel_ms": direct_ms,
-                  "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3)},
+                  "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3),
+                  # the setup add = the partitioned add pipeline (add_partitioned.hip), PMC per call
+                  "add_ms": add_ms,
+                  "add_traffic": load_traffic(args.traffic_json, "add_pipeline"),
+                  "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch")},
     }
     h.close()
     client.shutdown()
@@ -352,6 +385,7 @@ def run_c3(args, world, rank, local):
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
     present = int(counts.sum().item()) / max(args.warmup + args.steps, 1)
+    peak = gather_peak(client, 4 << 30, n, 4, stream, g)  # random gathers over a table far past the caches
     algo = n * (16 + k * 8)
     achieved = algo / (ms / 1e3) / 1e9
     res = {
@@ -365,7 +399,8 @@ def run_c3(args, world, rank, local):
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, "k_bloom_contains_multi"),
-                     "kernel": "k_bloom_contains_multi<16,16,4>", "kernel_avg_ms": ms},
+                     "kernel": "k_bloom_contains_multi<16,16,4>", "kernel_avg_ms": ms,
+                     **request_fields(args.traffic_json, "k_bloom_contains_multi", ms, peak)},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
     for h in handles:
@@ -437,6 +472,7 @@ def run_c5(args, world, rank, local):
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
     top = int(torch.bincount(kf.long(), minlength=nt).max().item())
+    peak = gather_peak(client, 4 << 30, n, 4, stream, g)
     res = {
         "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
         "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -448,8 +484,10 @@ def run_c5(args, world, rank, local):
                    "tenants_this_gpu": nt, "ops_per_gpu": n, "hottest_tenant_ops": top,
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": n * (64 + 10 * 8) / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": n * (64 + 10 * 8) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms},
+                     "unit": "GB/s", "frac": n * (64 + 10 * 8) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.traffic_json, "stream_pipeline"),
+                     "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms,
+                     **request_fields(args.traffic_json, "stream_pipeline", ms, peak)},
     }
     for h in handles:
         h.close()

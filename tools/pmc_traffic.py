@@ -21,6 +21,10 @@ import re
 
 SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_bk_probe", r"k_bk_probe"),
          ("k_bk_final", r"k_bk_final"),
+         ("k_ba_stage1", r"k_ba_stage1<"), ("k_ba_rebucket", r"k_ba_rebucket"), ("k_ba_region", r"k_ba_region"),
+         ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
+         ("k_stream_probe", r"k_stream_probe<"), ("k_stream_contains", r"k_stream_contains<"),
+         ("k_stream_commit", r"k_stream_commit<"),
          ("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains", r"k_bloom_contains<"),
          ("k_bloom_add_probe", r"k_bloom_add_probe"), ("k_bloom_add_commit", r"k_bloom_add_commit"),
          ("k_gather_probe", r"k_gather_probe"), ("k_hll_pfadd", r"k_hll_pfadd"), ("k_hll_count", r"k_hll_count"),
@@ -48,12 +52,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("-o", default="profiles/traffic.json")
+    ap.add_argument("--calls", nargs="*", default=[],
+                    help="pipeline=N: API calls of that pipeline in the profiled run (per-call totals)")
     a = ap.parse_args()
+    calls = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.calls}
     merged = collections.defaultdict(dict)
+    launches = {}
     for d in a.dirs:
         for k, cs in load(d).items():
             for c, v in cs.items():
                 merged[k][c] = sum(v) / len(v)
+                launches[k] = len(v)
     out = {}
     for k, cs in merged.items():
         fetch = cs.get("FETCH_SIZE")
@@ -74,14 +83,22 @@ def main():
             # memory requests at the L2 -> EA interface (the binding rate for these kernels)
             e["requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"] + cs["TCC_EA0_WRREQ_sum"]
         out[k] = e
-    # the partitioned contains is one call = these kernels in sequence: sum per call
-    pipe = [k for k in ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_final") if k in out]
-    if pipe:
-        agg = {"kernels": pipe}
+    for k in out:
+        out[k]["launches_profiled"] = launches.get(k)
+    # one API call = these kernels in sequence, possibly once per chunk: per-call totals =
+    # all profiled launches' counters / the calls in the profiled run (--calls)
+    for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_final")),
+                        ("add_pipeline", ("k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys", "k_ba_final")),
+                        ("stream_pipeline", ("k_stream_probe", "k_stream_contains", "k_stream_commit"))):
+        if not all(k in out for k in parts) or name not in calls:
+            continue
+        agg = {"kernels": list(parts), "calls_profiled": calls[name],
+               "note": "per API call: sum over the profiled launches / calls (the keys "
+                       "written '_per_launch' here mean per call)"}
         for f in ("hbm_bytes_per_launch", "requests_per_launch", "fetch_bytes_x2", "write_bytes"):
-            if all(f in out[k] for k in pipe):
-                agg[f] = sum(out[k][f] for k in pipe)
-        out["contains_pipeline"] = agg
+            if all(f in out[k] for k in parts):
+                agg[f] = sum(out[k][f] * launches[k] for k in parts) / calls[name]
+        out[name] = agg
     os.makedirs(os.path.dirname(a.o) or ".", exist_ok=True)
     with open(a.o, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
