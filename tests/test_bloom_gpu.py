@@ -703,3 +703,37 @@ def test_cross_stream_calls_run_in_call_order(client, fresh):
         assert c[0] >= n * 0.999  # in-batch false positives of the smaller filter (~1e-4 at its end fill)
         h.close()
         f.delete()
+
+
+def test_default_partitioned_paths_device_keys(client, fresh):
+    """Default dispatch on device-resident keys at C2 geometry (2^32 bits, k = 7), 4.5M 32-byte
+    keys -- above both partitioned paths' thresholds: per-key add flags and contains flags from
+    the partitioned pipelines equal the oracle's, and so do the exported bitmap bytes."""
+    import torch
+
+    from redisson_amd import device_keys
+
+    rng = np.random.default_rng(0x5EED00C2)
+    n = 4_500_000
+    first = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    probe = np.concatenate([first[: n // 2], rng.integers(0, 256, size=(n - n // 2, 32), dtype=np.uint8)])
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 32, 7)
+    h = BloomHandle(client, fresh)
+    ref = O.OracleBloom(1 << 32, 7)
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    d_first = torch.from_numpy(first).cuda()
+    d_probe = torch.from_numpy(probe).cuda()
+    d_new = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    d_pres = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the uploads ran on torch's stream, the engine uses its own
+    h.add_dev(device_keys(d_first.data_ptr(), n, 32), cnt.data_ptr(), d_out=d_new.data_ptr())
+    h.contains_dev(device_keys(d_probe.data_ptr(), n, 32), cnt.data_ptr() + 8, d_out=d_pres.data_ptr())
+    torch.cuda.synchronize()
+    cr, nr = ref.add(*O.fixed_arena(first), per_key=True)
+    pr_c, pr = ref.contains(*O.fixed_arena(probe), per_key=True)
+    assert int(cnt[0].item()) == cr and np.array_equal(d_new.cpu().numpy(), nr)
+    assert int(cnt[1].item()) == pr_c and np.array_equal(d_pres.cpu().numpy(), pr)
+    assert f.exportBitmap() == ref.redis_string()
+    h.close()
+    f.delete()
