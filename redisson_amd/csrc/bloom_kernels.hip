@@ -410,47 +410,88 @@ __device__ __forceinline__ uint32_t ht_find(const HTEntry *__restrict__ T, uint3
 }
 
 // ---- ordered mixed stream (C5): key i is a single-key contains (op 0) or add (op 1) on
-// filters[kf[i]], executed in key order.  Per chunk: probe the adds (first-setter table of
-// add positions per initially-zero bit), then the contains -- a zero bit counts as set iff an
-// add at an earlier position of the chunk touches it -- then commit the adds.  Earlier chunks
-// are committed before later ones probe, so chunking keeps the order.
+// filters[kf[i]], executed in key order.  Per chunk: compact the adds' positions, probe the adds
+// (first-setter table of add positions per initially-zero bit, plus a prefilter bitset of the
+// (filter, bit) pairs they touch), then the contains -- a zero bit counts as set iff an add at
+// an earlier position of the chunk touches it; the table is consulted only when the prefilter
+// bit is set -- then commit the adds.  Earlier chunks are committed before later ones probe, so
+// chunking keeps the order.  The add list is unordered: owners are resolved by atomicMin.
+constexpr uint32_t kPrefilterBits = 25;  // 4 MiB: mostly L2-resident while the contains run
+
+__device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx) {
+    return (uint32_t)(((((uint64_t)fid << 32) | idx) * 0x9E3779B97F4A7C15ULL) >> (64 - kPrefilterBits));
+}
+
+// adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
+__global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restrict__ op, uint64_t base, uint64_t nchunk,
+                                                        uint32_t *__restrict__ adds, uint32_t *__restrict__ nadds) {
+    __shared__ uint32_t s_cnt, s_base;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = (1ULL << lane) - 1;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * 1024; t0 < nchunk; t0 += (uint64_t)gridDim.x * 1024) {
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        bool a[4];
+        uint32_t pos[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t t = t0 + q * 256 + threadIdx.x;
+            a[q] = t < nchunk && op[base + t];
+            const uint64_t mask = __ballot(a[q]);
+            uint32_t wb = 0;
+            if (lane == 0 && mask) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
+            pos[q] = __shfl(wb, 0, 64) + (uint32_t)__popcll(mask & lt);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(nadds, s_cnt) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (a[q]) adds[s_base + pos[q]] = (uint32_t)(t0 + q * 256 + threadIdx.x);
+        __syncthreads();
+    }
+}
+
 template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t base, uint64_t nchunk,
+__global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t base, const uint32_t *__restrict__ adds,
+                                                      const uint32_t *__restrict__ nadds,
                                                       const FilterDesc *__restrict__ filt,
-                                                      const uint32_t *__restrict__ kf, const uint8_t *__restrict__ op,
-                                                      HTEntry *__restrict__ T, uint32_t log2cap, uint32_t epoch,
-                                                      uint32_t *__restrict__ zmask) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+                                                      const uint32_t *__restrict__ kf, HTEntry *__restrict__ T,
+                                                      uint32_t log2cap, uint32_t epoch, uint32_t *__restrict__ zmask,
+                                                      uint32_t *__restrict__ prefilter) {
+    const uint32_t na = *nadds;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
+        const uint32_t t = adds[a];
         const uint64_t i = base + t;
         uint32_t zm = 0;
-        if (op[i]) {
-            const FilterDesc f = filt[kf[i]];
-            uint64_t h1, h2;
-            hash_key<KLEN>(keys, i, h1, h2);
-            uint32_t word[KMAX], idxs[KMAX];
-            uint32_t maxidx = 0;
-            uint64_t h = h1;
+        const FilterDesc f = filt[kf[i]];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint32_t maxidx = 0;
+        uint64_t h = h1;
 #pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if ((uint32_t)j < f.k) {
-                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                    idxs[j] = idx;
-                    word[j] = f.bm[idx >> 5];
-                    maxidx = idx > maxidx ? idx : maxidx;
-                }
-                h += (j & 1) ? h1 : h2;
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
             }
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
-                    zm |= 1u << j;
-                    ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], (uint32_t)t);
-                }
-            }
-            raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+            h += (j & 1) ? h1 : h2;
         }
-        zmask[t] = zm;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+                zm |= 1u << j;
+                ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], t);
+                const uint32_t pb = prefilter_bit(f.fid, idxs[j]);
+                atomicOr(&prefilter[pb >> 5], 1u << (pb & 31));
+            }
+        }
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+        zmask[a] = zm;
     }
 }
 
@@ -460,7 +501,8 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
                                                          const uint32_t *__restrict__ kf,
                                                          const uint8_t *__restrict__ op,
                                                          const HTEntry *__restrict__ T, uint32_t log2cap,
-                                                         uint32_t epoch, uint8_t *__restrict__ out,
+                                                         uint32_t epoch, const uint32_t *__restrict__ prefilter,
+                                                         uint8_t *__restrict__ out,
                                                          unsigned long long *__restrict__ counts) {
     uint64_t present = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -489,8 +531,14 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
 #pragma unroll
             for (int u = 0; u < KMAX; ++u) {
                 if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
-                    const uint32_t owner = ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
-                    all = owner < (uint32_t)t;  // set by an earlier add of this chunk
+                    // set by an earlier add of this chunk?  Only possible if the prefilter says so.
+                    const uint32_t pb = prefilter_bit(f.fid, idxs[u]);
+                    if ((prefilter[pb >> 5] >> (pb & 31)) & 1u) {
+                        const uint32_t owner = ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
+                        all = owner < (uint32_t)t;
+                    } else {
+                        all = false;
+                    }
                 }
             }
             j = e;
@@ -502,19 +550,20 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
 }
 
 template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t base, uint64_t nchunk,
+__global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t base, const uint32_t *__restrict__ adds,
+                                                       const uint32_t *__restrict__ nadds,
                                                        const FilterDesc *__restrict__ filt,
-                                                       const uint32_t *__restrict__ kf,
-                                                       const uint8_t *__restrict__ op, const HTEntry *__restrict__ T,
+                                                       const uint32_t *__restrict__ kf, const HTEntry *__restrict__ T,
                                                        uint32_t log2cap, uint32_t epoch,
                                                        const uint32_t *__restrict__ zmask, uint8_t *__restrict__ out,
                                                        unsigned long long *__restrict__ counts) {
     uint64_t added = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+    const uint32_t na = *nadds;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
+        const uint32_t t = adds[a];
         const uint64_t i = base + t;
-        if (!op[i]) continue;
-        const uint32_t zm = zmask[t];
+        const uint32_t zm = zmask[a];
         bool isnew = false;
         if (zm) {
             const FilterDesc f = filt[kf[i]];
@@ -525,7 +574,7 @@ __global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t ba
             for (int j = 0; j < KMAX; ++j) {
                 if ((zm >> j) & 1u) {
                     const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                    if (ht_owner(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx) == (uint32_t)t) {
+                    if (ht_owner(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idx) == t) {
                         isnew = true;
                         atomicOr(&f.bm[idx >> 5], bit_in_word(idx));
                     }
@@ -862,12 +911,15 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(a.nchunk, kMaxGrid);
-    hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.zmask);
+    const unsigned cgrid = (unsigned)std::min<uint64_t>((a.nchunk + 1023) / 1024, 2048);
+    hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
+                       a.nadds);
+    hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter);
     hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.out, a.counts);
-    hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
+                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out, a.counts);
+    hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
 }
 
 template <int KLEN>

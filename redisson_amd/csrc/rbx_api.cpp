@@ -185,6 +185,7 @@ struct rbx_ctx {
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits;  // partitioned add
+    DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
@@ -1407,11 +1408,18 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, (1ULL << 26) / k));
     RBX_TRY(c->zmask.reserve(chunk * 4));
+    RBX_TRY(c->st_adds.reserve(chunk * 4));
+    constexpr uint64_t kPrefilterWords = 1ULL << (25 - 5);  // bloom_kernels.hip kPrefilterBits
+    RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
         RBX_TRY(ensure_table(c, nch * k, st));
+        HIP_TRY(hipMemsetAsync(c->st_prefilter.p, 0, (kPrefilterWords + 1) * 4, st));
         StreamChunkArgs s{};
+        s.adds = c->st_adds.as<uint32_t>();
+        s.prefilter = c->st_prefilter.as<uint32_t>();
+        s.nadds = s.prefilter + kPrefilterWords;
         s.keys = keys;
         s.base = base;
         s.nchunk = nch;

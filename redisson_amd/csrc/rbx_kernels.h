@@ -116,10 +116,13 @@ struct StreamChunkArgs {
     const uint8_t *op;    // per key: 0 contains, 1 add
     HTEntry *table;
     uint32_t log2cap, epoch;
-    uint32_t *zmask;
+    uint32_t *zmask;      // per add-list entry
     uint32_t kmax;
     uint8_t *out;         // per key: present (contains) / newly added (add)
     unsigned long long *counts;  // [0] present contains, [1] new adds
+    uint32_t *adds;       // nchunk: compacted chunk-local positions of the adds
+    uint32_t *nadds;      // 1, zeroed per chunk
+    uint32_t *prefilter;  // 2^25 bits, zeroed per chunk
 };
 
 // bloom_kernels.hip
