@@ -126,6 +126,22 @@ int rbx_bloom_is_exists(rbx_ctx *ctx, const char *name, int *exists);
 /* rename :349-364 and renamenx :366-385 */
 int rbx_bloom_rename(rbx_ctx *ctx, const char *name, const char *new_name);
 int rbx_bloom_renamenx(rbx_ctx *ctx, const char *name, const char *new_name, int *renamed);
+
+/* ---- key timeouts: RExpirable (M/RedissonExpirable.java:53-251) ----------------------------
+ * Keys are removed lazily once their timeout passes (Redis semantics); handles follow their name.
+ * rbx_pexpire replaces expireAsync / expireAtAsync (:207-239): PEXPIRE (absolute = 0, when_ms
+ * relative) or PEXPIREAT (absolute = 1, unix ms) on every key, *result = 1 iff any timeout was
+ * set.  cond: 0 none, 1 NX, 2 XX, 3 GT, 4 LT (expireIfNotSet / expireIfSet / expireIfGreater /
+ * expireIfLess).  RBloomFilter passes {name, "{name}:config"} (M/RedissonBloomFilter.java:303-310),
+ * RHyperLogLog {name}. */
+int rbx_pexpire(rbx_ctx *ctx, const char *const *names, uint32_t n, int64_t when_ms, int absolute, int cond,
+                int *result);
+/* clearExpireAsync (:241-251): PERSIST every key, *result = 1 iff any timeout was removed */
+int rbx_persist(rbx_ctx *ctx, const char *const *names, uint32_t n, int *result);
+/* remainTimeToLiveAsync (:193-195) = PTTL, getExpireTimeAsync (:203-205) = PEXPIRETIME of one key:
+ * -2 when the key does not exist, -1 when it has no timeout */
+int rbx_pttl(rbx_ctx *ctx, const char *name, int64_t *out);
+int rbx_pexpiretime(rbx_ctx *ctx, const char *name, int64_t *out);
 /* GET name: the Redis bitmap string (MSB-first, length = highest SETBIT byte + 1).
  * Writes min(cap, len) bytes; *redis_len = len. */
 int rbx_bloom_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap, uint64_t *redis_len);

@@ -71,6 +71,10 @@ SIGNATURES = {
     "rbx_bloom_is_exists": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
     "rbx_bloom_rename": (C.c_int, [vp, C.c_char_p, C.c_char_p]),
     "rbx_bloom_renamenx": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.POINTER(C.c_int)]),
+    "rbx_pexpire": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+    "rbx_persist": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_pttl": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
+    "rbx_pexpiretime": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
     "rbx_bloom_export": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64, u64p]),
     "rbx_bloom_import": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64]),
     "rbx_bloom_import_dev": (C.c_int, [vp, C.c_char_p, vp, C.c_uint64, vp]),

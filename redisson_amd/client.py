@@ -78,7 +78,71 @@ class RedissonClient:
         self.shutdown()
 
 
-class RBloomFilter:
+def _config_name(name: str) -> str:
+    """suffixName(name, "config") (M/RedissonObject.java): the config hash shares the name's slot."""
+    return name + ":config" if "{" in name else "{" + name + "}:config"
+
+
+class _Expirable:
+    """RExpirable (M/RedissonExpirable.java:53-251) over rbx_pexpire / rbx_persist / rbx_pttl.
+    Times are milliseconds; `_expire_keys()` lists the keys a timeout applies to."""
+
+    _COND = {None: 0, "NX": 1, "XX": 2, "GT": 3, "LT": 4}
+
+    def _pexpire(self, when_ms: int, absolute: bool, cond=None) -> bool:
+        keys = [k.encode() for k in self._expire_keys()]
+        arr = (C.c_char_p * len(keys))(*keys)
+        r = C.c_int()
+        _check(L.lib().rbx_pexpire(self._client.ctx, arr, len(keys), int(when_ms), int(absolute), self._COND[cond],
+                                   C.byref(r)))
+        return bool(r.value)
+
+    def expire(self, ttl_ms: int) -> bool:
+        """expire(Duration) :118-125 -- PEXPIRE on every key"""
+        return self._pexpire(ttl_ms, False)
+
+    def expireAt(self, unix_ms: int) -> bool:
+        """expireAt(long) :58-65 -- PEXPIREAT"""
+        return self._pexpire(unix_ms, True)
+
+    def expireIfSet(self, ttl_ms: int) -> bool:
+        """:138-145 -- PEXPIRE .. XX"""
+        return self._pexpire(ttl_ms, False, "XX")
+
+    def expireIfNotSet(self, ttl_ms: int) -> bool:
+        """:148-155 -- PEXPIRE .. NX"""
+        return self._pexpire(ttl_ms, False, "NX")
+
+    def expireIfGreater(self, ttl_ms: int) -> bool:
+        """PEXPIRE .. GT"""
+        return self._pexpire(ttl_ms, False, "GT")
+
+    def expireIfLess(self, ttl_ms: int) -> bool:
+        """PEXPIRE .. LT"""
+        return self._pexpire(ttl_ms, False, "LT")
+
+    def clearExpire(self) -> bool:
+        """clearExpireAsync :183-185 / :241-251 -- PERSIST"""
+        keys = [k.encode() for k in self._expire_keys()]
+        arr = (C.c_char_p * len(keys))(*keys)
+        r = C.c_int()
+        _check(L.lib().rbx_persist(self._client.ctx, arr, len(keys), C.byref(r)))
+        return bool(r.value)
+
+    def remainTimeToLive(self) -> int:
+        """:188-195 -- PTTL name (-2 missing, -1 no timeout)"""
+        out = C.c_int64()
+        _check(L.lib().rbx_pttl(self._client.ctx, self._expire_keys()[0].encode(), C.byref(out)))
+        return int(out.value)
+
+    def getExpireTime(self) -> int:
+        """:198-205 -- PEXPIRETIME name"""
+        out = C.c_int64()
+        _check(L.lib().rbx_pexpiretime(self._client.ctx, self._expire_keys()[0].encode(), C.byref(out)))
+        return int(out.value)
+
+
+class RBloomFilter(_Expirable):
     """M/RedissonBloomFilter.java.  size/hashIterations are cached like the reference's
     volatile fields (:61-62) and re-validated on every batch (addConfigCheck :207-213)."""
 
@@ -187,6 +251,10 @@ class RBloomFilter:
         _check(L.lib().rbx_bloom_is_exists(self._client.ctx, self._bname(), C.byref(e)))
         return bool(e.value)
 
+    def _expire_keys(self):
+        # M/RedissonBloomFilter.java:303-314: the bitmap and its config hash
+        return [self._name, _config_name(self._name)]
+
     def rename(self, newName: str) -> None:
         _check(L.lib().rbx_bloom_rename(self._client.ctx, self._bname(), newName.encode()))
         self._name = newName
@@ -290,7 +358,7 @@ def bloom_stream(client: RedissonClient, handles: list[BloomHandle], key_filter,
     return out[: arena.n], counts
 
 
-class RHyperLogLog:
+class RHyperLogLog(_Expirable):
     """M/RedissonHyperLogLog.java (PFADD / PFCOUNT / PFMERGE)."""
 
     def __init__(self, client: RedissonClient, name: str, codec: Codec):
@@ -338,6 +406,9 @@ class RHyperLogLog:
         e = C.c_int()
         _check(L.lib().rbx_hll_exists(self._client.ctx, self._name.encode(), C.byref(e)))
         return bool(e.value)
+
+    def _expire_keys(self):
+        return [self._name]
 
     def exportDense(self) -> bytes:
         """GET name, as the Redis dense HLL string."""

@@ -153,20 +153,26 @@ struct Entry {
     std::shared_ptr<BloomConfig> cfg;
     std::shared_ptr<Bitmap> bm;
     std::shared_ptr<HllState> hll;
+    int64_t expire_at = -1;  // unix ms of the key's timeout (PEXPIREAT), -1 = persistent
 };
 
+// Handles are bound to a NAME, like a Redisson object: a call re-resolves the keys whenever the
+// keyspace changed since the handle's last call (gen), so delete / rename / expire / re-import
+// behave as they do through the name-based entry points.
 struct rbx_bloom {
     rbx_ctx *ctx;
     std::string name;
     uint64_t size;
     uint32_t k;
     std::shared_ptr<Bitmap> bm;
+    uint64_t gen = 0;
 };
 
 struct rbx_hll {
     rbx_ctx *ctx;
     std::string name;
     std::shared_ptr<HllState> st;
+    uint64_t gen = 0;
 };
 
 struct rbx_ctx {
@@ -190,7 +196,8 @@ struct rbx_ctx {
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
     uint64_t filt_generation = 0;
-    uint64_t generation = 1;  // bumped whenever a bitmap is (re)allocated or freed
+    uint64_t generation = 1;  // bumped whenever a key is created / removed or a bitmap (re)allocated
+    int64_t next_expiry = INT64_MAX;  // earliest expire_at in the keyspace (an upper bound)
 
     std::shared_ptr<SlabPool> slab = std::make_shared<SlabPool>();
 
@@ -426,10 +433,42 @@ static uint64_t read_dev_u64(rbx_ctx *c, const unsigned long long *p, int *rc) {
     return v;
 }
 
-// exact-match lookups
+static int64_t now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (int64_t)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+// exact-match lookups; a key past its timeout is removed on access (Redis lazy expiry)
 static Entry *find(rbx_ctx *c, const std::string &k) {
     auto it = c->ks.find(k);
-    return it == c->ks.end() ? nullptr : &it->second;
+    if (it == c->ks.end()) return nullptr;
+    if (it->second.expire_at >= 0 && it->second.expire_at <= now_ms()) {
+        c->ks.erase(it);
+        c->generation++;
+        return nullptr;
+    }
+    return &it->second;
+}
+
+// removes every key past its timeout once the earliest timeout has passed (so handle-based
+// calls, which skip the name lookup while nothing changed, still see expirations)
+static void expire_sweep(rbx_ctx *c) {
+    if (c->next_expiry == INT64_MAX) return;
+    const int64_t now = now_ms();
+    if (now < c->next_expiry) return;
+    int64_t next = INT64_MAX;
+    for (auto it = c->ks.begin(); it != c->ks.end();) {
+        const int64_t t = it->second.expire_at;
+        if (t >= 0 && t <= now) {
+            it = c->ks.erase(it);
+            c->generation++;
+            continue;
+        }
+        if (t >= 0) next = std::min(next, t);
+        ++it;
+    }
+    c->next_expiry = next;
 }
 
 // =====================================================================================
@@ -1138,8 +1177,8 @@ int rbx_bloom_delete(rbx_ctx *c, const char *name, int *deleted) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
     int n = 0;
-    n += (int)c->ks.erase(name);
-    n += (int)c->ks.erase(config_name(name));
+    if (find(c, name)) n += (int)c->ks.erase(name);
+    if (find(c, config_name(name))) n += (int)c->ks.erase(config_name(name));
     if (n) c->generation++;
     if (deleted) *deleted = n;
     return RBX_OK;
@@ -1154,11 +1193,11 @@ int rbx_bloom_is_exists(rbx_ctx *c, const char *name, int *exists) {
 
 // RENAME semantics: overwrite the target; missing source -> "ERR no such key"
 static int ks_rename(rbx_ctx *c, const std::string &from, const std::string &to) {
-    auto it = c->ks.find(from);
-    if (it == c->ks.end()) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
+    Entry *src = find(c, from);
+    if (!src) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
     if (from == to) return RBX_OK;
-    Entry e = it->second;
-    c->ks.erase(it);
+    Entry e = *src;  // RENAME keeps the timeout
+    c->ks.erase(from);
     c->ks[to] = e;
     c->generation++;
     return RBX_OK;
@@ -1274,7 +1313,7 @@ int rbx_bloom_open(rbx_ctx *c, const char *name, rbx_bloom **out) {
     std::shared_ptr<Bitmap> bm;
     RBX_TRY(bitmap_for(c, name, cfg->size, true, &bm));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    *out = new rbx_bloom{c, name, cfg->size, cfg->k, bm};
+    *out = new rbx_bloom{c, name, cfg->size, cfg->k, bm, c->generation};
     return RBX_OK;
 }
 
@@ -1294,6 +1333,26 @@ int rbx_bloom_handle_config(const rbx_bloom *b, uint64_t *size, uint32_t *k) {
 
 static KeysDev keys_dev(const rbx_keys *k) { return KeysDev{k->bytes, k->offsets, k->stride, k->n}; }
 
+// Re-resolves a Bloom handle's keys if the keyspace changed since its last call: the config
+// must still hold the handle's (size, k) (addConfigCheck, M/RedissonBloomFilter.java:207-213) and
+// the handle follows whatever bitmap the name holds now; *absent: no bitmap (GETBIT reads 0s).
+static int bloom_bind(rbx_ctx *c, rbx_bloom *b, bool create, bool *absent) {
+    expire_sweep(c);
+    *absent = false;
+    if (b->gen == c->generation) return RBX_OK;
+    RBX_TRY(config_check(c, b->name, b->size, b->k));
+    std::shared_ptr<Bitmap> bm;
+    RBX_TRY(bitmap_for(c, b->name, b->size, create, &bm));
+    if (!bm) {
+        *absent = true;
+        return RBX_OK;
+    }
+    b->bm = bm;
+    b->gen = c->generation;
+    return RBX_OK;
+}
+
+
 int rbx_bloom_contains_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out,
                            unsigned long long *d_count, void *stream) {
     if (!c || !b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
@@ -1302,6 +1361,12 @@ int rbx_bloom_contains_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uin
     std::lock_guard<std::recursive_mutex> g(c->mu);
     ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
+    bool absent;
+    RBX_TRY(bloom_bind(c, b, false, &absent));
+    if (absent) {  // GETBIT on a missing key: every bit is 0 (the count is unchanged)
+        if (d_out) HIP_TRY(hipMemsetAsync(d_out, 0, d_keys->n, pick_stream(c, stream)));
+        return RBX_OK;
+    }
     KeysDev k = keys_dev(d_keys);
     FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
     return run_contains(c, k, f, d_out, d_count, pick_stream(c, stream));
@@ -1315,6 +1380,8 @@ int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t 
     std::lock_guard<std::recursive_mutex> g(c->mu);
     ScratchOrder so_(c, pick_stream(c, stream));
     RBX_TRY(set_device(c));
+    bool absent;
+    RBX_TRY(bloom_bind(c, b, true, &absent));
     KeysDev k = keys_dev(d_keys);
     FilterDesc f = desc_of(*b->bm, b->size, b->k, 0);
     return run_add(c, k, nullptr, nullptr, 0, f, b->k, d_out_new, d_count, nullptr, pick_stream(c, stream));
@@ -1325,9 +1392,14 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
     std::vector<FilterDesc> v(nseg);
     std::unordered_map<const Bitmap *, uint32_t> fid;
     uint32_t km = 1;
+    expire_sweep(c);
     for (uint32_t s = 0; s < nseg; ++s) {
         rbx_bloom *b = filters[s];
         if (!b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL filter handle");
+        if (b->gen != c->generation) {  // (a missing bitmap is created: the kernels need one)
+            bool absent;
+            RBX_TRY(bloom_bind(c, b, true, &absent));
+        }
         auto it = fid.find(b->bm.get());
         uint32_t id = it == fid.end() ? (uint32_t)fid.size() : it->second;
         if (it == fid.end()) fid[b->bm.get()] = id;
@@ -1547,8 +1619,21 @@ static int hll_get(rbx_ctx *c, const std::string &name, bool create, std::shared
     h->owner = c;
     h->card = 0;  // createHLLObject: cached cardinality 0, valid
     c->ks[name] = Entry{KType::Hll, nullptr, nullptr, h};
+    c->generation++;
     *out = h;
     if (created) *created = true;
+    return RBX_OK;
+}
+
+// HLL handles follow the name too; PFADD on a missing key creates it (createHLLObject), PFCOUNT
+// reads it as empty (h->st = null) without creating it
+static int hll_bind(rbx_ctx *c, rbx_hll *h, bool create) {
+    expire_sweep(c);
+    if (h->gen == c->generation && h->st) return RBX_OK;
+    std::shared_ptr<HllState> st;
+    RBX_TRY(hll_get(c, h->name, create, &st, nullptr));
+    h->st = st;
+    if (st) h->gen = c->generation;
     return RBX_OK;
 }
 
@@ -1890,11 +1975,13 @@ int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t 
     std::lock_guard<std::recursive_mutex> g(c->mu);
     ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
-    auto it = c->ks.find(name);
+    Entry *ex = find(c, name);
     std::shared_ptr<HllState> h;
-    if (it != c->ks.end() && it->second.type == KType::Hll) {
-        h = it->second.hll;
+    if (ex && ex->type == KType::Hll) {
+        h = ex->hll;
+        ex->expire_at = -1;  // SET discards the timeout
     } else {
+        c->generation++;
         h = std::make_shared<HllState>();
         RBX_TRY(hll_alloc(c, &h->d_regs));
         h->owner = c;
@@ -1911,7 +1998,8 @@ int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t 
 int rbx_hll_delete(rbx_ctx *c, const char *name, int *deleted) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(c->mu);
-    int n = (int)c->ks.erase(name);
+    int n = find(c, name) ? (int)c->ks.erase(name) : 0;
+    if (n) c->generation++;
     if (deleted) *deleted = n;
     return RBX_OK;
 }
@@ -1931,7 +2019,7 @@ int rbx_hll_open(rbx_ctx *c, const char *name, int create, rbx_hll **out) {
     RBX_TRY(hll_get(c, name, create != 0, &h, nullptr));
     if (!h) return fail(RBX_E_NO_SUCH_KEY, "ERR no such key");
     HIP_TRY(hipStreamSynchronize(c->stream));
-    *out = new rbx_hll{c, name, h};
+    *out = new rbx_hll{c, name, h, c->generation};
     return RBX_OK;
 }
 
@@ -1945,6 +2033,8 @@ int rbx_hll_close(rbx_hll *h) {
 
 int rbx_hll_registers_dev(rbx_hll *h, void **d_regs) {
     if (!h || !d_regs) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(h->ctx->mu);
+    RBX_TRY(hll_bind(h->ctx, h, true));
     *d_regs = h->st->d_regs;
     return RBX_OK;
 }
@@ -1961,6 +2051,7 @@ int rbx_hll_add_multi_dev(rbx_ctx *c, rbx_hll *const *hlls, uint32_t nseg, const
     std::vector<HllState *> hl(nseg);
     for (uint32_t s = 0; s < nseg; ++s) {
         if (!hlls[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL hll handle");
+        RBX_TRY(hll_bind(c, hlls[s], true));
         hl[s] = hlls[s]->st.get();
         hl[s]->card |= 1ULL << 63;  // conservatively invalidate (the flags are device-side)
     }
@@ -1973,7 +2064,10 @@ int rbx_hll_count_each_handles(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n, uin
     ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
     std::vector<HllState *> hl(n);
-    for (uint32_t i = 0; i < n; ++i) hl[i] = hlls[i] ? hlls[i]->st.get() : nullptr;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (hlls[i]) RBX_TRY(hll_bind(c, hlls[i], false));
+        hl[i] = hlls[i] ? hlls[i]->st.get() : nullptr;
+    }
     return pfcount_each(c, hl, out);
 }
 
@@ -2006,6 +2100,10 @@ int rbx_hll_allreduce_max(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n) {
     ScratchOrder so_(c, c->stream);
     if (!c->comm) return fail(RBX_E_ILLEGAL_STATE, "rbx_rccl_init has not been called");
     RBX_TRY(set_device(c));
+    for (uint32_t t = 0; t < n; ++t) {
+        if (!hlls[t]) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL hll handle");
+        RBX_TRY(hll_bind(c, hlls[t], true));
+    }
     // coalesce runs of adjacent register blocks into one all-reduce each
     uint32_t i = 0;
     ncclGroupStart();
@@ -2118,6 +2216,76 @@ int rbx_set_staging(rbx_ctx *c, uint64_t bytes) {
     if (!c || bytes < 4096) return fail(RBX_E_ILLEGAL_ARGUMENT, "staging must be >= 4 KiB");
     std::lock_guard<std::recursive_mutex> g(c->mu);
     c->staging_bytes = bytes;
+    return RBX_OK;
+}
+
+// ---- key timeouts (RedissonExpirable, M/RedissonExpirable.java:53-251) ----------------------
+// PEXPIRE / PEXPIREAT over several keys with the Lua fold of expireAsync / expireAtAsync
+// (:207-239): result = 1 iff the timeout of any key was set.  Redis 7.2 rules per key: a
+// missing key gives 0; cond NX = only without a timeout, XX = only with one, GT / LT = only if
+// the new time is later / earlier (a key without a timeout counts as infinite); a time not in
+// the future deletes the key (and counts as set).
+int rbx_pexpire(rbx_ctx *c, const char *const *names, uint32_t n, int64_t when_ms, int absolute, int cond,
+                int *result) {
+    if (!c || (n && !names) || cond < 0 || cond > 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    const int64_t now = now_ms();
+    const int64_t at = absolute ? when_ms : now + when_ms;
+    int any = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!names[i]) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key name");
+        Entry *e = find(c, names[i]);
+        if (!e) continue;
+        const int64_t cur = e->expire_at;  // -1: persistent (infinite for GT / LT)
+        if (cond == 1 && cur >= 0) continue;
+        if (cond == 2 && cur < 0) continue;
+        if (cond == 3 && (cur < 0 || at <= cur)) continue;
+        if (cond == 4 && cur >= 0 && at >= cur) continue;
+        any = 1;
+        if (at <= now) {
+            c->ks.erase(names[i]);
+            c->generation++;
+            continue;
+        }
+        e->expire_at = at;
+        c->next_expiry = std::min(c->next_expiry, at);
+    }
+    if (result) *result = any;
+    return RBX_OK;
+}
+
+// PERSIST over several keys (clearExpireAsync :241-251): result = 1 iff any timeout was removed
+int rbx_persist(rbx_ctx *c, const char *const *names, uint32_t n, int *result) {
+    if (!c || (n && !names)) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    int any = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!names[i]) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key name");
+        Entry *e = find(c, names[i]);
+        if (e && e->expire_at >= 0) {
+            e->expire_at = -1;
+            any = 1;
+        }
+    }
+    if (result) *result = any;
+    return RBX_OK;
+}
+
+// PTTL (remainTimeToLiveAsync :193-195) and PEXPIRETIME (getExpireTimeAsync :203-205) of one
+// key: -2 when the key does not exist, -1 when it has no timeout
+int rbx_pttl(rbx_ctx *c, const char *name, int64_t *out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Entry *e = find(c, name);
+    *out = !e ? -2 : e->expire_at < 0 ? -1 : std::max<int64_t>(0, e->expire_at - now_ms());
+    return RBX_OK;
+}
+
+int rbx_pexpiretime(rbx_ctx *c, const char *name, int64_t *out) {
+    if (!c || !name || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Entry *e = find(c, name);
+    *out = !e ? -2 : e->expire_at;
     return RBX_OK;
 }
 

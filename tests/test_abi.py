@@ -81,3 +81,12 @@ def test_error_mapping_without_gpu():
         assert "greater than 1" in str(e)
     rc = L.lib().rbx_bloom_optimal_config(100, 0.03, C.byref(s), C.byref(k))
     assert rc == 0 and (s.value, k.value) == (729, 5)
+
+
+def test_ttl_symbols_declared():
+    """The key-timeout entry points are exported and declared (RExpirable surface)."""
+    import re
+
+    hdr = open(os.path.join(ROOT, "include", "rbx.h")).read()
+    for sym in ("rbx_pexpire", "rbx_persist", "rbx_pttl", "rbx_pexpiretime"):
+        assert re.search(r"\b%s\(" % sym, hdr), sym
