@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librbx.so")
+LIB_PATH = os.environ.get("RBX_LIB_PATH") or os.path.join(_HERE, "librbx.so")  # override: A/B runs only
 
 u8p = C.POINTER(C.c_uint8)
 u64p = C.POINTER(C.c_uint64)

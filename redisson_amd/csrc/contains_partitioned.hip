@@ -54,6 +54,30 @@ __device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, ui
     }
 }
 
+// Region pairs (emit2 -> probe) are 6 bytes, split into two arrays: lo = offset in the region
+// (19 bits) << 13 | key bits 0-12, hi = key bits 13-26 (chunks hold < 2^27 keys).  Against 8-byte
+// pairs this saves a quarter of emit2's write requests and of the probe's read requests.
+constexpr uint32_t kBkKeyLoBits = 13;
+static_assert(kBkRegionBits + kBkKeyLoBits == 32, "lo word = region offset | low key bits");
+
+__device__ __forceinline__ void bk_write_run6(const unsigned long long *s_img, uint32_t st, uint32_t n, uint64_t gb,
+                                              uint32_t *__restrict__ lo, uint16_t *__restrict__ hi, uint64_t cap,
+                                              uint32_t lane, const uint32_t *__restrict__ bm,
+                                              unsigned long long *__restrict__ miss) {
+    for (uint32_t t = lane; t < n; t += 64) {
+        const unsigned long long e = s_img[st + t];
+        const uint64_t gp = gb + t;
+        if (gp < cap) {
+            const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
+            __builtin_nontemporal_store(((idx & ((1u << kBkRegionBits) - 1)) << kBkKeyLoBits) |
+                                            (key & ((1u << kBkKeyLoBits) - 1)), lo + gp);
+            __builtin_nontemporal_store((uint16_t)(key >> kBkKeyLoBits), hi + gp);
+        } else {
+            bk_direct(e, bm, miss);
+        }
+    }
+}
+
 // K1 -----------------------------------------------------------------------------------
 // Tile = NT * PER keys.  Hash, test bit 0 (one random gather per key), then the survivors'
 // k-1 remaining bits are counted per coarse bucket in LDS, scanned, placed bucket-sorted in an
@@ -156,7 +180,8 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
                                                   const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
                                                   uint32_t items_per_c, uint32_t fb, uint32_t nregions, uint64_t cap2,
-                                                  unsigned long long *__restrict__ pairs2, uint32_t *__restrict__ cnt2,
+                                                  uint32_t *__restrict__ p2lo, uint16_t *__restrict__ p2hi,
+                                                  uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
                                                   uint32_t flags) {
     constexpr int PER = 8;  // uint4 (two pairs) per thread
@@ -213,30 +238,33 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
         __syncthreads();
         for (uint32_t f = wave; f < nf; f += NT / 64) {
             const uint32_t n = s_cnt[f];
-            bk_write_run(s_img, s_start[f], n, s_gb[f], pairs2 + (uint64_t)((c << fb) + f) * cap2, cap2, lane, bm, miss);
+            const uint64_t rb = (uint64_t)((c << fb) + f) * cap2;
+            bk_write_run6(s_img, s_start[f], n, s_gb[f], p2lo + rb, p2hi + rb, cap2, lane, bm, miss);
         }
         __syncthreads();
     }
 }
 
 // K4 -----------------------------------------------------------------------------------
-__device__ __forceinline__ void bk_test(const uint32_t *s_bm, unsigned long long e, unsigned long long *miss,
-                                        uint32_t flags) {
-    const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
-    if ((s_bm[(idx & ((1u << kBkRegionBits) - 1)) >> 5] & bit_in_word(idx)) == 0u) {
+__device__ __forceinline__ void bk_test6(const uint32_t *s_bm, uint32_t lo, uint32_t hi, unsigned long long *miss,
+                                         uint32_t flags) {
+    const uint32_t off = lo >> kBkKeyLoBits;
+    if ((s_bm[off >> 5] & bit_in_word(off)) == 0u) {  // regions are word-aligned: off's low bits = idx's
+        const uint32_t key = (hi << kBkKeyLoBits) | (lo & ((1u << kBkKeyLoBits) - 1));
         if (flags & 8) miss[0] = 0;  // diagnostics: one fixed store instead of the scattered atomic
         else atomicOr(&miss[key >> 6], 1ULL << (key & 63));
     }
 }
 
-// One block per region; pairs are read as uint4 (two pairs), 8 per lane per round trip,
-// the first round issued together with the region's bitmap load.
-__global__ __launch_bounds__(1024) void k_bk_probe(const unsigned long long *__restrict__ pairs2,
+// One block per region; a lane reads 4 pairs at a time (16 B of lo words + 8 B of hi halves),
+// 6 groups per round trip, the first round issued together with the region's bitmap load.
+__global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ p2lo,
+                                                   const uint16_t *__restrict__ p2hi,
                                                    const uint32_t *__restrict__ cnt2, uint64_t cap2, uint32_t nregions,
                                                    const uint32_t *__restrict__ bm, uint64_t nwords4,
                                                    unsigned long long *__restrict__ miss, uint32_t flags) {
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
-    constexpr uint32_t NT = 1024;
+    constexpr uint32_t NT = 1024, G = 6;
     for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
         const uint32_t n = (uint32_t)min<uint64_t>(cnt2[r], cap2);
         if (n == 0) continue;  // uniform
@@ -250,14 +278,19 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const unsigned long long *__r
             const uint32_t j = i * NT + threadIdx.x;
             if (j < nv) b[i] = srcv[j];
         }
-        // cap2 is a multiple of 64 pairs: the region's pairs are 16-byte aligned
-        const u32x4 *src = (const u32x4 *)(pairs2 + (uint64_t)r * cap2);
-        const uint32_t n2 = (n + 1) >> 1;
-        u32x4 v[8];
+        // cap2 is a multiple of 64 pairs: the region's lo words are 16-byte and hi halves 8-byte aligned
+        const u32x4 *slo = (const u32x4 *)(p2lo + (uint64_t)r * cap2);
+        const u32x2 *shi = (const u32x2 *)(p2hi + (uint64_t)r * cap2);
+        const uint32_t n4 = (n + 3) >> 2;
+        u32x4 vl[G];
+        u32x2 vh[G];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (uint32_t u = 0; u < G; ++u) {
             const uint32_t q = u * NT + threadIdx.x;
-            if (q < n2) v[u] = __builtin_nontemporal_load(src + q);
+            if (q < n4) {
+                vl[u] = __builtin_nontemporal_load(slo + q);
+                vh[u] = __builtin_nontemporal_load(shi + q);
+            }
         }
 #pragma unroll
         for (uint32_t i = 0; i < kBkRegionWords / 4 / NT; ++i) {
@@ -267,19 +300,25 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const unsigned long long *__r
         __syncthreads();
         for (uint32_t base = 0;;) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < G; ++u) {
                 const uint32_t q = base + u * NT + threadIdx.x;
-                if (q < n2) {
-                    bk_test(s_bm, w2(v[u].x, v[u].y), miss, flags);
-                    if (2 * q + 1 < n) bk_test(s_bm, w2(v[u].z, v[u].w), miss, flags);
+                if (q < n4) {
+                    const uint32_t p0 = 4 * q;
+                    bk_test6(s_bm, vl[u].x, vh[u].x & 0xffffu, miss, flags);
+                    if (p0 + 1 < n) bk_test6(s_bm, vl[u].y, vh[u].x >> 16, miss, flags);
+                    if (p0 + 2 < n) bk_test6(s_bm, vl[u].z, vh[u].y & 0xffffu, miss, flags);
+                    if (p0 + 3 < n) bk_test6(s_bm, vl[u].w, vh[u].y >> 16, miss, flags);
                 }
             }
-            base += 8 * NT;
-            if (base >= n2) break;
+            base += G * NT;
+            if (base >= n4) break;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < G; ++u) {
                 const uint32_t q = base + u * NT + threadIdx.x;
-                if (q < n2) v[u] = __builtin_nontemporal_load(src + q);
+                if (q < n4) {
+                    vl[u] = __builtin_nontemporal_load(slo + q);
+                    vh[u] = __builtin_nontemporal_load(shi + q);
+                }
             }
         }
         __syncthreads();  // s_bm reuse
@@ -330,14 +369,14 @@ static void bk_emit2(const PcArgs &a, hipStream_t st) {
     // cap1 is a multiple of 64 pairs and of every tile size used here (>= 16 * 256)
     const uint32_t items_per_c = (uint32_t)((a.cap1 + 16 * NT2 - 1) / (16 * NT2));
     hipLaunchKernelGGL((k_bk_emit2<NT2>), dim3(2048), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1, a.ncoarse,
-                       items_per_c, a.fb, a.nregions, a.cap2, a.pairs2, a.cnt2, a.bm, a.miss, a.flags);
+                       items_per_c, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
 }
 
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
     bk_stage1<KLEN, KMAX, 512>(a, st);
     bk_emit2<512>(a, st);
-    hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.pairs2, a.cnt2,
+    hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
                        a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.flags);
     hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,
                        a.out, a.count);

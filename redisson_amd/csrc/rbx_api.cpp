@@ -745,7 +745,7 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
     while ((1ULL << lg) < nregions) ++lg;
     const uint32_t fb = lg > 6 ? lg - 6 : 0;
     const uint32_t ncoarse = (nregions + (1u << fb) - 1) >> fb;
-    // keys per chunk: key ids fit 32 bits and a chunk's pairs stay <= 2^30
+    // keys per chunk: key ids fit 27 bits (6-byte region pairs) and a chunk's pairs stay <= 2^30
     uint64_t chunk = std::min<uint64_t>(1ULL << 27, (1ULL << 30) / (k - 1));
     const uint64_t nch = (keys.n + chunk - 1) / chunk;
     chunk = (keys.n + nch - 1) / nch;
@@ -763,7 +763,7 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
     const uint64_t ncnt = 64 * kBkSub + (uint64_t)nregions;  // cnt1 (padded), cnt2
     RBX_TRY(c->pc_cnt.reserve(ncnt * 4));
     RBX_TRY(c->pc_pairs1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
-    RBX_TRY(c->pc_pairs2.reserve((uint64_t)nregions * cap2 * 8));
+    RBX_TRY(c->pc_pairs2.reserve((uint64_t)nregions * cap2 * 6));  // 6-byte region pairs (lo u32 + hi u16)
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         PcArgs a{};
@@ -785,7 +785,8 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
         a.cnt1 = c->pc_cnt.as<uint32_t>();
         a.cnt2 = a.cnt1 + 64 * kBkSub;
         a.pairs1 = c->pc_pairs1.as<unsigned long long>();
-        a.pairs2 = c->pc_pairs2.as<unsigned long long>();
+        a.p2lo = c->pc_pairs2.as<uint32_t>();
+        a.p2hi = (uint16_t *)(a.p2lo + (uint64_t)nregions * cap2);
         a.out = d_out;
         a.count = d_count;
         a.flags = (uint32_t)g_partition_flags;

@@ -70,7 +70,8 @@ struct PcArgs {
     unsigned long long *alive;  // ceil(nchunk/64)
     unsigned long long *miss;   // ceil(nchunk/64), zeroed
     unsigned long long *pairs1; // ncoarse * kBkSub * cap1
-    unsigned long long *pairs2; // nregions * cap2
+    uint32_t *p2lo;         // nregions * cap2: region offset << 13 | key bits 0-12
+    uint16_t *p2hi;         // nregions * cap2: key bits 13-26
     uint8_t *out;
     unsigned long long *count;
     uint32_t flags;  // diagnostics only (rbx_tune "contains_partition_flags"); 0 in normal operation

@@ -238,6 +238,8 @@ def main():
         torch.cuda.synchronize()
         dk = device_keys(keys.data_ptr(), n, 32)
         variants = [(0, 0), (1, 0), (1, 4), (1, 8)]  # flags 4, 8: diagnostics (wrong results, timing only)
+        if os.environ.get("RBX_PFLAGS"):  # e.g. "1:0,1:16": A/B of experimental switches
+            variants = [tuple(int(x) for x in v.split(":")) for v in os.environ["RBX_PFLAGS"].split(",")]
         res = {v: [] for v in variants}
         counts = {}
         for rnd in range(5):
