@@ -204,8 +204,18 @@ int rbx_hll_count(rbx_ctx *ctx, const char *const *names, uint32_t n, uint64_t *
 int rbx_hll_count_each(rbx_ctx *ctx, const char *const *names, uint32_t n, uint64_t *out);
 /* mergeWith -> PFMERGE dest src1..srcn (dest's registers included)  :97-102 */
 int rbx_hll_merge(rbx_ctx *ctx, const char *dest, const char *const *srcs, uint32_t nsrc);
-/* GET name: Redis dense HLL string (16-byte "HYLL" header + 12288 bytes) */
+/* GET name: Redis dense HLL string (16-byte "HYLL" header + 12288 bytes).  *len = 0 if absent. */
 int rbx_hll_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap, uint64_t *len);
+/* GET name in a chosen encoding ([redis-7.2] hyperloglog.c):
+ *   RBX_HLL_DENSE      the dense string (as rbx_hll_export);
+ *   RBX_HLL_SPARSE     ZERO / XZERO / VAL opcodes, fewest bytes; ILLEGAL_ARGUMENT if a register > 32;
+ *   RBX_HLL_AS_STORED  the encoding Redis would hold: PFADD creates sparse strings, promoted to
+ *                      dense (one way) when a register exceeds 32 or the string would exceed
+ *                      hll-sparse-max-bytes (3000); SET keeps the imported encoding; PFMERGE's
+ *                      destination is dense iff it or any source is.
+ * *len receives the full length; at most cap bytes are copied. */
+enum { RBX_HLL_DENSE = 0, RBX_HLL_SPARSE = 1, RBX_HLL_AS_STORED = 2 };
+int rbx_hll_export_enc(rbx_ctx *ctx, const char *name, int encoding, uint8_t *out, uint64_t cap, uint64_t *len);
 /* SET name <Redis HLL string> (dense or sparse encoding) */
 int rbx_hll_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint64_t len);
 int rbx_hll_delete(rbx_ctx *ctx, const char *name, int *deleted);

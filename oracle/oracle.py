@@ -265,6 +265,58 @@ def hll_dense_pack(regs: np.ndarray) -> bytes:
     return out[:12288].tobytes()
 
 
+# Redis sparse HLL opcodes [redis-7.2 hyperloglog.c, "sparse representation" comment block]:
+#   ZERO  00xxxxxx           run of 1..64 zero registers
+#   XZERO 01xxxxxx yyyyyyyy  run of 1..16384 zero registers (14-bit length - 1)
+#   VAL   1vvvvvxx           run of 1..4 registers holding value 1..32
+def hll_sparse_pack(regs: np.ndarray) -> bytes | None:
+    """Fewest-bytes sparse opcode string of the registers (no header); None if a register > 32."""
+    out = bytearray()
+    r = np.asarray(regs, dtype=np.uint8)
+    i = 0
+    while i < 16384:
+        v = int(r[i])
+        j = i + 1
+        while j < 16384 and r[j] == v:
+            j += 1
+        run = j - i
+        if v == 0:
+            if run > 64:
+                out += bytes([0x40 | ((run - 1) >> 8), (run - 1) & 0xFF])
+            else:
+                out.append(run - 1)
+        else:
+            if v > 32:
+                return None
+            while run:
+                n = min(run, 4)
+                out.append(0x80 | ((v - 1) << 2) | (n - 1))
+                run -= n
+        i = j
+    return bytes(out)
+
+
+def hll_sparse_unpack(ops: bytes) -> np.ndarray:
+    """Registers of a sparse opcode string (no header); ValueError unless it covers 16384."""
+    out = hll_new()
+    i = p = 0
+    while p < len(ops):
+        b = ops[p]
+        if b & 0xC0 == 0:
+            i, p = i + (b & 0x3F) + 1, p + 1
+        elif b & 0xC0 == 0x40:
+            i, p = i + (((b & 0x3F) << 8) | ops[p + 1]) + 1, p + 2
+        else:
+            n = (b & 3) + 1
+            out[i:i + n] = ((b >> 2) & 0x1F) + 1
+            i, p = i + n, p + 1
+        if i > 16384:
+            raise ValueError("sparse string overruns 16384 registers")
+    if i != 16384:
+        raise ValueError("sparse string covers %d registers" % i)
+    return out
+
+
 def hll_dense_unpack(data: bytes) -> np.ndarray:
     src = np.zeros(12289, np.uint8)
     src[:12288] = np.frombuffer(data[:12288], np.uint8)

@@ -96,6 +96,7 @@ SIGNATURES = {
     "rbx_hll_merge": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32]),
     "rbx_hll_export": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64, u64p]),
     "rbx_hll_import": (C.c_int, [vp, C.c_char_p, u8p, C.c_uint64]),
+    "rbx_hll_export_enc": (C.c_int, [vp, C.c_char_p, C.c_int, u8p, C.c_uint64, u64p]),
     "rbx_hll_delete": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
     "rbx_hll_exists": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
     "rbx_hll_open": (C.c_int, [vp, C.c_char_p, C.c_int, C.POINTER(vp)]),

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _lib as L
 from .codec import DEFAULT_CODEC, Codec
-from .exceptions import raise_for
+from .exceptions import IllegalArgumentException, raise_for
 from .keys import Arena
 
 
@@ -416,6 +416,20 @@ class RHyperLogLog(_Expirable):
         buf = np.zeros(16 + 12288, np.uint8)
         _check(L.lib().rbx_hll_export(self._client.ctx, self._name.encode(), buf.ctypes.data_as(L.u8p),
                                       buf.size, C.byref(n)))
+        return buf[: n.value].tobytes()
+
+    _ENCODINGS = {"dense": 0, "sparse": 1, "stored": 2}
+
+    def exportString(self, encoding: str = "stored") -> bytes:
+        """GET name as a Redis HLL string: "stored" = the encoding Redis would hold (sparse until
+        promoted), "dense", or "sparse" (IllegalArgumentException if a register exceeds 32).
+        Empty bytes if the key does not exist."""
+        if encoding not in self._ENCODINGS:
+            raise IllegalArgumentException("encoding must be one of %s" % sorted(self._ENCODINGS))
+        n = C.c_uint64()
+        buf = np.zeros(16 + 12288, np.uint8)
+        _check(L.lib().rbx_hll_export_enc(self._client.ctx, self._name.encode(), self._ENCODINGS[encoding],
+                                          buf.ctypes.data_as(L.u8p), buf.size, C.byref(n)))
         return buf[: n.value].tobytes()
 
     def importString(self, data: bytes) -> None:

@@ -142,6 +142,7 @@ struct Bitmap {  // a Redis string used with SETBIT/GETBIT
 struct HllState {  // a Redis HLL string, registers unpacked (1 byte each) on the device
     uint8_t *d_regs = nullptr;  // 16384 bytes inside a pool chunk
     uint64_t card = 0;          // the header's 8 cached-cardinality bytes (LE); bit 63 = invalid
+    bool dense = false;         // Redis encoding: created sparse, promoted to dense once (never back)
     struct rbx_ctx *owner = nullptr;
     ~HllState();
 };
@@ -1891,6 +1892,7 @@ int rbx_hll_merge(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_
     }
     std::shared_ptr<HllState> d;
     RBX_TRY(hll_get(c, dest, true, &d, nullptr));
+    for (auto &h : keep) d->dense = d->dense || h->dense;  // pfmergeCommand: use_dense if any input is
     if (!sp.empty()) {
         RBX_TRY(c->ptrs.reserve(sp.size() * sizeof(uint8_t *)));
         HIP_TRY(hipMemcpyAsync(c->ptrs.p, sp.data(), sp.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
@@ -1902,9 +1904,60 @@ int rbx_hll_merge(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_
     return RBX_OK;
 }
 
-// Redis dense encoding (HLL_DENSE_SET_REGISTER layout), 16-byte header
-int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *len) {
+// Redis HLL strings: 16-byte header ("HYLL", encoding, 3 unused, 8 cached-cardinality bytes)
+// + dense registers (HLL_DENSE_SET_REGISTER layout, 6 bits each, LSB-first) or sparse opcodes.
+constexpr uint64_t kHllDenseLen = 16 + 12288;
+constexpr uint64_t kHllSparseMaxBytes = 3000;  // redis.conf hll-sparse-max-bytes (default)
+
+static void hll_header(uint8_t *s, int sparse, uint64_t card) {
+    memcpy(s, "HYLL", 4);
+    s[4] = (uint8_t)sparse;  // HLL_DENSE 0 / HLL_SPARSE 1
+    s[5] = s[6] = s[7] = 0;
+    for (int i = 0; i < 8; ++i) s[8 + i] = (uint8_t)(card >> (8 * i));
+}
+
+static void hll_encode_dense(const uint8_t *regs, uint8_t *p) {
+    memset(p, 0, 12288);
+    for (unsigned long r = 0; r < 16384; ++r) {
+        const unsigned long byte = r * 6 / 8, fb = r * 6 & 7, fb8 = 8 - fb, v = regs[r];
+        p[byte] |= (uint8_t)(v << fb);
+        if (byte + 1 < 12288) p[byte + 1] |= (uint8_t)(v >> fb8);
+    }
+}
+
+// Sparse opcodes with the fewest bytes: zero runs as ZERO (<= 64) or XZERO (65..16384), equal
+// values as VAL runs of <= 4 (value 1..32).  Returns false when a register exceeds 32 (the
+// sparse format cannot hold it).  Redis builds its sparse string incrementally (hllSparseSet);
+// zero runs come out identical, runs of one value may be split differently (4+1 vs 1+4), with
+// the same registers.
+static bool hll_encode_sparse(const uint8_t *regs, std::vector<uint8_t> &out) {
+    out.clear();
+    for (uint32_t i = 0; i < 16384;) {
+        const uint8_t v = regs[i];
+        uint32_t j = i + 1;
+        while (j < 16384 && regs[j] == v) ++j;
+        uint32_t run = j - i;
+        if (v == 0) {
+            if (run > 64) {
+                out.push_back((uint8_t)(0x40 | ((run - 1) >> 8)));
+                out.push_back((uint8_t)((run - 1) & 0xff));
+            } else {
+                out.push_back((uint8_t)(run - 1));
+            }
+        } else {
+            if (v > 32) return false;
+            for (; run; run -= std::min<uint32_t>(run, 4))
+                out.push_back((uint8_t)(0x80 | ((v - 1) << 2) | (std::min<uint32_t>(run, 4) - 1)));
+        }
+        i = j;
+    }
+    return true;
+}
+
+int rbx_hll_export_enc(rbx_ctx *c, const char *name, int encoding, uint8_t *out, uint64_t cap, uint64_t *len) {
     if (!c || !name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    if (encoding < RBX_HLL_DENSE || encoding > RBX_HLL_AS_STORED)
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "encoding must be RBX_HLL_DENSE, RBX_HLL_SPARSE or RBX_HLL_AS_STORED");
     std::lock_guard<std::recursive_mutex> g(c->mu);
     ScratchOrder so_(c, c->stream);
     RBX_TRY(set_device(c));
@@ -1917,21 +1970,34 @@ int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uin
     std::vector<uint8_t> regs(kHllBytes);
     HIP_TRY(hipMemcpyAsync(regs.data(), h->d_regs, kHllBytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::vector<uint8_t> s(16 + 12288 + 1, 0);
-    memcpy(s.data(), "HYLL", 4);
-    s[4] = 0;  // HLL_DENSE
-    for (int i = 0; i < 8; ++i) s[8 + i] = (uint8_t)(h->card >> (8 * i));
-    uint8_t *p = s.data() + 16;
-    for (unsigned long r = 0; r < 16384; ++r) {
-        unsigned long byte = r * 6 / 8, fb = r * 6 & 7, fb8 = 8 - fb, v = regs[r];
-        p[byte] &= (uint8_t)~(63UL << fb);
-        p[byte] |= (uint8_t)(v << fb);
-        p[byte + 1] &= (uint8_t)~(63UL >> fb8);
-        p[byte + 1] |= (uint8_t)(v >> fb8);
+    std::vector<uint8_t> s;
+    bool sparse = false;
+    if (encoding == RBX_HLL_SPARSE || (encoding == RBX_HLL_AS_STORED && !h->dense)) {
+        std::vector<uint8_t> ops;
+        const bool fits = hll_encode_sparse(regs.data(), ops);
+        if (encoding == RBX_HLL_SPARSE && !fits)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "a register exceeds 32: not representable in the sparse encoding");
+        // hllSparseSet promotes once a value exceeds 32 or the string exceeds hll-sparse-max-bytes
+        if (fits && (encoding == RBX_HLL_SPARSE || 16 + ops.size() <= kHllSparseMaxBytes)) {
+            s.resize(16 + ops.size());
+            memcpy(s.data() + 16, ops.data(), ops.size());
+            sparse = true;
+        } else {
+            h->dense = true;  // promotion is one-way
+        }
     }
-    if (len) *len = 16 + 12288;
-    if (out) memcpy(out, s.data(), std::min<uint64_t>(cap, 16 + 12288));
+    if (!sparse) {
+        s.resize(kHllDenseLen);
+        hll_encode_dense(regs.data(), s.data() + 16);
+    }
+    hll_header(s.data(), sparse, h->card);
+    if (len) *len = s.size();
+    if (out) memcpy(out, s.data(), std::min<uint64_t>(cap, s.size()));
     return RBX_OK;
+}
+
+int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uint64_t *len) {
+    return rbx_hll_export_enc(c, name, RBX_HLL_DENSE, out, cap, len);
 }
 
 // accepts the Redis dense and sparse encodings (isHLLObjectOrReply validation)
@@ -1941,7 +2007,7 @@ int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t 
     if (len < 16 || memcmp(bytes, "HYLL", 4) != 0 || bytes[4] > 1) return fail(RBX_E_WRONGTYPE, bad);
     std::vector<uint8_t> regs(kHllBytes, 0);
     if (bytes[4] == 0) {
-        if (len != 16 + 12288) return fail(RBX_E_WRONGTYPE, bad);
+        if (len != kHllDenseLen) return fail(RBX_E_WRONGTYPE, bad);
         const uint8_t *p = bytes + 16;
         for (unsigned long r = 0; r < 16384; ++r) {
             unsigned long byte = r * 6 / 8, fb = r * 6 & 7, fb8 = 8 - fb;
@@ -1991,6 +2057,7 @@ int rbx_hll_import(rbx_ctx *c, const char *name, const uint8_t *bytes, uint64_t 
     uint64_t card = 0;
     for (int i = 0; i < 8; ++i) card |= (uint64_t)bytes[8 + i] << (8 * i);
     h->card = card;
+    h->dense = bytes[4] == 0;  // SET keeps the string's encoding
     HIP_TRY(hipMemcpyAsync(h->d_regs, regs.data(), kHllBytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RBX_OK;

@@ -158,3 +158,18 @@ def test_hll_estimator_accuracy():
         regs = O.hll_new()
         O.hll_pfadd(regs, *O.fixed_arena(rng.integers(0, 256, size=(n, 16), dtype=np.uint8)))
         assert abs(O.hll_count(regs) - n) / n < 0.03
+
+
+def test_hll_sparse_pack_opcodes():
+    # [redis-7.2] hyperloglog.c opcodes: an empty HLL is one XZERO of 16384 registers
+    assert O.hll_sparse_pack(O.hll_new()) == b"\x7f\xff"
+    regs = O.hll_new()
+    regs[0:5] = 3        # VAL(3) x4 + VAL(3) x1
+    regs[69] = 32        # ZERO run of 64, VAL(32) x1, then XZERO of the rest
+    assert O.hll_sparse_pack(regs) == bytes([0x8B, 0x88, 0x3F, 0xFC, 0x40 | (16313 >> 8), 16313 & 0xFF])
+    regs[70] = 33
+    assert O.hll_sparse_pack(regs) is None
+    rng = np.random.default_rng(7)
+    for fill in (0.01, 0.2, 1.0):
+        r = np.where(rng.random(16384) < fill, rng.integers(1, 33, 16384), 0).astype(np.uint8)
+        assert np.array_equal(O.hll_sparse_unpack(O.hll_sparse_pack(r)), r)
