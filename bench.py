@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--tenants", type=int, default=100_000, help="C3 tenant count (whole node)")
     p.add_argument("--elements", type=int, default=1_000_000_000, help="C4 PFADD elements per step per GPU")
     p.add_argument("--stage1", type=int, default=None, help="contains early-exit schedule (rbx_tune)")
+    p.add_argument("--tune", default="", help="extra rbx_tune settings for experiments: key=value,key=value")
     p.add_argument("--zipf-s", type=float, default=1.0, help="C5 tenant skew")
     p.add_argument("--add-fraction", type=float, default=0.1, help="C5 share of add commands")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
@@ -591,6 +592,11 @@ def main():
         from redisson_amd import _lib as L
 
         assert L.lib().rbx_tune(b"contains_stage1", args.stage1) == 0
+    for kv in filter(None, args.tune.split(",")):
+        from redisson_amd import _lib as L
+
+        key, val = kv.split("=")
+        assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
     log(f"[bench] rank {rank}/{world} workload {args.workload}")
     if args.workload == "c2":
         res = run_c2(args, world, rank, local)

@@ -255,6 +255,173 @@ __global__ __launch_bounds__(256) void k_bloom_contains_multi(KeysDev keys, cons
 }
 
 // ---------------------------------------------------------------------------------
+// contains with per-lane key slots (rbx_tune("contains_stage1", 5))
+// ---------------------------------------------------------------------------------
+// Each lane keeps P keys in flight and tests ONE bit per key per round trip, so a key costs
+// exactly as many gathers as the bits read before its first 0 (~2 on a filter at fill 0.5,
+// the minimum) while the lane still has P independent gathers outstanding.  A key that
+// finishes frees its slot; free slots are refilled, in key order, from a per-wave queue that the
+// whole wave fills convergently (hash, segment, first bit index of 64*Q consecutive keys, one
+// coalesced pass) -- so the divergent part is only a 32-byte LDS read.  Two queue buffers per
+// wave: while one is consumed the other holds the next range.  Results are identical to the
+// staged kernels (same bits, same AND); only the number of gathers changes.
+template <int KLEN, bool MULTI, int P, int Q>
+__global__ __launch_bounds__(256) void k_bloom_contains_q(KeysDev keys, const FilterDesc *__restrict__ filt,
+                                                          const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                          const uint32_t *__restrict__ tile_seg0, FilterDesc single,
+                                                          uint8_t *__restrict__ out,
+                                                          unsigned long long *__restrict__ counts) {
+    constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
+    struct alignas(16) QEnt {
+        uint64_t h1, h2;
+        const uint32_t *bm;
+        uint32_t seg, idx0;
+    };
+    __shared__ QEnt s_q[WAVES][2][RANGE];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    QEnt *qb = &s_q[wave][0][0];
+    const uint64_t nkeys = keys.n;
+    const uint64_t nranges = (nkeys + RANGE - 1) / RANGE;
+    const uint64_t ntiles = (nkeys + 255) >> 8;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    uint64_t rnext = (uint64_t)blockIdx.x * WAVES + wave;  // next range this wave hashes
+    uint64_t qbase[2] = {0, 0};
+    uint32_t qlen[2] = {0, 0};
+    auto fill = [&](uint32_t b) {  // wave-uniform: hash range rnext into buffer b
+        qlen[b] = 0;
+        if (rnext >= nranges) return;
+        const uint64_t rb = rnext * RANGE;
+        qbase[b] = rb;
+        qlen[b] = (uint32_t)min<uint64_t>(RANGE, nkeys - rb);
+#pragma unroll
+        for (uint32_t q = 0; q < Q; ++q) {
+            const uint32_t pos = q * 64 + lane;
+            const uint64_t i = rb + pos;
+            if (i < nkeys) {
+                QEnt e;
+                hash_key<KLEN>(keys, i, e.h1, e.h2);
+                e.seg = 0;
+                ModParams mp = single.mp;
+                e.bm = single.bm;
+                if constexpr (MULTI) {
+                    const uint64_t t = i >> 8;
+                    uint32_t lo = tile_seg0[t];
+                    uint32_t hi = t + 1 < ntiles ? tile_seg0[t + 1] + 1 : nseg;
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (seg_off[mid] <= i) lo = mid;
+                        else hi = mid;
+                    }
+                    e.seg = lo;
+                    mp = filt[lo].mp;
+                    e.bm = filt[lo].bm;
+                }
+                e.idx0 = mod63(e.h1 & 0x7fffffffffffffffULL, mp);
+                qb[b * RANGE + pos] = e;
+            }
+        }
+        rnext += nw;
+        __builtin_amdgcn_wave_barrier();
+    };
+    bool act[P];
+    uint64_t sh1[P], sh2[P], sh[P];
+    uint32_t si[P], sjk[P], sseg[P], sidx[P];  // key index (< 2^32, host-checked), j | k << 16
+    const uint32_t *sbm[P];
+    ModC smp[P];
+    const ModC single_mc = mod_compact(single.mp);
+#pragma unroll
+    for (int s = 0; s < P; ++s) act[s] = false;
+    uint32_t cur = 0, qpos = 0;
+    int stale = -1;  // a consumed buffer, refilled after the next gathers are issued
+    fill(0);
+    fill(1);
+    uint64_t present = 0;
+    for (;;) {
+        // refill free slots in key order (lanes by rank)
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            bool need = !act[s];
+            for (;;) {
+                const uint64_t nm = __ballot(need);
+                if (!nm) break;
+                if (qpos >= qlen[cur]) {
+                    if (stale == (int)(cur ^ 1)) {  // both buffers consumed in one refill: fill now
+                        fill(cur ^ 1);
+                        stale = -1;
+                    }
+                    if (qlen[cur ^ 1] == 0) break;  // queue exhausted
+                    stale = (int)cur;
+                    cur ^= 1;
+                    qpos = 0;
+                    continue;
+                }
+                const uint32_t avail = qlen[cur] - qpos;
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
+                if (need && rank < avail) {
+                    const QEnt e = qb[cur * RANGE + qpos + rank];
+                    act[s] = true;
+                    need = false;
+                    sh1[s] = e.h1;
+                    sh2[s] = e.h2;
+                    sh[s] = e.h1 + e.h2;  // hash 1 (h advances by h2 after j = 0)
+                    si[s] = (uint32_t)(qbase[cur] + qpos + rank);
+                    sidx[s] = e.idx0;
+                    sbm[s] = e.bm;
+                    sseg[s] = e.seg;
+                    if constexpr (MULTI) {  // needed only after the first gather returns
+                        smp[s] = mod_compact(filt[e.seg].mp);
+                        sjk[s] = filt[e.seg].k << 16;
+                    } else {
+                        sjk[s] = single.k << 16;
+                    }
+                }
+                qpos += min<uint32_t>((uint32_t)__popcll(nm), avail);
+            }
+        }
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < P; ++s) any |= act[s];
+        if (!__ballot(any)) break;  // every slot drained and the queue is empty
+        uint32_t w[P];
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+            if (act[s]) w[s] = sbm[s][sidx[s] >> 5];
+        if (stale >= 0) {  // hash the next range while this round's gathers are in flight
+            fill((uint32_t)stale);
+            stale = -1;
+        }
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            bool fin_p = false;
+            if (act[s]) {
+                bool fin = false;
+                if ((w[s] & bit_in_word(sidx[s])) == 0u) {
+                    fin = true;
+                } else if (((++sjk[s]) & 0xffffu) >= (sjk[s] >> 16)) {
+                    fin = fin_p = true;
+                } else {
+                    sidx[s] = mod63c(sh[s] & 0x7fffffffffffffffULL, MULTI ? smp[s] : single_mc);
+                    sh[s] += (sjk[s] & 1) ? sh1[s] : sh2[s];
+                }
+                if (fin) {
+                    act[s] = false;
+                    if (out) out[si[s]] = fin_p;
+                }
+            }
+            if constexpr (MULTI) {
+                if (counts && __ballot(fin_p)) wave_seg_add(fin_p, sseg[s], 1u, counts);
+            } else {
+                present += fin_p;
+            }
+        }
+    }
+    if constexpr (!MULTI) {
+        if (counts) block_add_u64(present, counts);
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // add: first-setter table
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t ht_slot(uint64_t keypart, uint32_t log2cap) {
@@ -799,9 +966,43 @@ static void launch_contains_s(const KeysDev &keys, const uint32_t *bm, const Mod
     hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
 }
 
+static unsigned g_qgrid = 2048;  // slot kernel grid (grid-stride over 64*Q-key ranges)
+static int g_qshape = 22;        // slot kernel: P * 10 + Q (slots per lane, queue keys per lane)
+void set_contains_qshape(int v) { g_qshape = v; }
+void set_contains_qgrid(int v) { g_qgrid = (unsigned)v; }
+
+template <int KLEN, bool MULTI>
+static void launch_contains_q(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off, uint32_t nseg,
+                              const uint32_t *tile_seg0, const FilterDesc &single, uint8_t *out,
+                              unsigned long long *counts, hipStream_t st, unsigned grid) {
+    const dim3 g(std::min(grid, g_qgrid)), b(256);
+#define RBX_Q(P, Q) hipLaunchKernelGGL((k_bloom_contains_q<KLEN, MULTI, P, Q>), g, b, 0, st, keys, filt, seg_off, nseg, \
+                                       tile_seg0, single, out, counts)
+    if constexpr (KLEN == 16) {
+        switch (g_qshape) {
+        case 24: RBX_Q(2, 4); return;
+        case 42: RBX_Q(4, 2); return;
+        case 32: RBX_Q(3, 2); return;
+        case 34: RBX_Q(3, 4); return;
+        case 44: RBX_Q(4, 4); return;
+        default: break;
+        }
+    }
+    RBX_Q(2, 2);
+#undef RBX_Q
+}
+
 template <int KLEN, int KMAX>
 static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
                                uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    if (g_stage1 == 5 && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
+        FilterDesc f{};
+        f.bm = const_cast<uint32_t *>(bm);
+        f.mp = mp;
+        f.k = k;
+        launch_contains_q<KLEN, false>(keys, nullptr, nullptr, 0u, nullptr, f, out, count, st, grid);
+        return;
+    }
     switch (g_stage1) {
     case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid); break;
     case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid); break;
@@ -833,8 +1034,12 @@ void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *b
 template <int KLEN>
 static void launch_contains_multi_k(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off,
                                     uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax, uint8_t *out,
-                                    unsigned long long *counts, hipStream_t st, unsigned grid) {
+                                    unsigned long long *counts, hipStream_t st, unsigned grid, bool slots) {
     const bool dbl = g_stage1 == 4;
+    if ((slots || g_stage1 == 5) && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
+        launch_contains_q<KLEN, true>(keys, filt, seg_off, nseg, tile_seg0, FilterDesc{}, out, counts, st, grid);
+        return;
+    }
     if (kmax <= 8) {
         if (dbl) hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 4>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
         else hipLaunchKernelGGL((k_bloom_contains_multi<KLEN, 8, 1>), dim3(grid), dim3(256), 0, st, keys, filt, seg_off, nseg, tile_seg0, out, counts);
@@ -855,13 +1060,13 @@ void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, ui
 
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
                                  const uint64_t *seg_off, uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax,
-                                 uint8_t *out, unsigned long long *counts, hipStream_t st) {
+                                 uint8_t *out, unsigned long long *counts, hipStream_t st, bool slots) {
     const unsigned grid = grid_for(keys.n, kMaxGrid);
     switch (klen_fast) {
-    case 16: launch_contains_multi_k<16>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
-    case 32: launch_contains_multi_k<32>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
-    case 64: launch_contains_multi_k<64>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
-    default: launch_contains_multi_k<0>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid); break;
+    case 16: launch_contains_multi_k<16>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid, slots); break;
+    case 32: launch_contains_multi_k<32>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid, slots); break;
+    case 64: launch_contains_multi_k<64>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid, slots); break;
+    default: launch_contains_multi_k<0>(keys, filt, seg_off, nseg, tile_seg0, kmax, out, counts, st, grid, slots); break;
     }
 }
 

@@ -1390,7 +1390,15 @@ int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t 
 }
 
 // Uploads the per-segment descriptor table (cached by content + bitmap generation).
-static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, uint32_t *kmax, hipStream_t st) {
+// Multi-tenant contains takes the per-lane slot kernel (one gather per key per round trip) when
+// the distinct bitmaps of a call exceed this many bytes (past the caches, the request count
+// binds); below it the staged kernel (fewer instructions per key) is faster.  rbx_tune
+// "contains_multi_slots": 0 never, 1 always, 2 by this threshold (default).
+static int g_multi_slots = 2;
+constexpr uint64_t kSlotsMinBytes = 64ULL << 20;
+
+static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, uint32_t *kmax, hipStream_t st,
+                          uint64_t *distinct_bytes = nullptr) {
     std::vector<FilterDesc> v(nseg);
     std::unordered_map<const Bitmap *, uint32_t> fid;
     uint32_t km = 1;
@@ -1404,7 +1412,10 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
         }
         auto it = fid.find(b->bm.get());
         uint32_t id = it == fid.end() ? (uint32_t)fid.size() : it->second;
-        if (it == fid.end()) fid[b->bm.get()] = id;
+        if (it == fid.end()) {
+            fid[b->bm.get()] = id;
+            if (distinct_bytes) *distinct_bytes += (b->size + 7) / 8;
+        }
         if (id >= (1u << 24)) return fail(RBX_E_ILLEGAL_ARGUMENT, "more than 2^24 distinct filters in one call");
         v[s] = desc_of(*b->bm, b->size, b->k, id);
         km = std::max(km, b->k);
@@ -1432,13 +1443,15 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     RBX_TRY(set_device(c));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
-    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
+    uint64_t bytes = 0;
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, &bytes));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
     RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
     launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+    const bool slots = g_multi_slots == 1 || (g_multi_slots == 2 && bytes >= kSlotsMinBytes);
     launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg,
-                                c->tile_segs.as<uint32_t>(), kmax, d_out, d_counts, st);
+                                c->tile_segs.as<uint32_t>(), kmax, d_out, d_counts, st, slots);
     HIP_TRY(hipGetLastError());
     return RBX_OK;
 }
@@ -2385,8 +2398,25 @@ int rbx_tune(const char *key, int value) {
         g_add_partition_mode = value;
         return RBX_OK;
     }
+    if (!strcmp(key, "contains_multi_slots")) {
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_multi_slots in [0, 2]");
+        g_multi_slots = value;
+        return RBX_OK;
+    }
+    // EXPERIMENTS (tools/microbench.py): shape and grid of the slot contains kernel (stage 5)
+    if (!strcmp(key, "contains_qshape")) {
+        if (value != 22 && value != 24 && value != 32 && value != 34 && value != 42 && value != 44)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qshape in {22, 24, 32, 34, 42, 44}");
+        set_contains_qshape(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "contains_qgrid")) {
+        if (value < 256 || value > 8192) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qgrid in [256, 8192]");
+        set_contains_qgrid(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_stage1")) {
-        if (value < 0 || value > 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1 in [0, 4]");
+        if (value < 0 || value > 5) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1 in [0, 5]");
         set_contains_stage1(value);
         return RBX_OK;
     }

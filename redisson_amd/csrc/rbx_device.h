@@ -72,6 +72,21 @@ RBX_HD uint32_t mod63(uint64_t h, const ModParams &p) {
     return r >> s;
 }
 
+// The fields mod63 reads, in 4 dwords (per-lane copies in register-heavy kernels).
+struct ModC {
+    uint32_t mask, sp, dn, v;  // sp = s | pow2 << 8
+};
+RBX_HD ModC mod_compact(const ModParams &p) { return ModC{p.mask, p.s | (p.pow2 << 8), p.dn, p.v}; }
+RBX_HD uint32_t mod63c(uint64_t h, const ModC &p) {
+    if (p.sp >> 8) return (uint32_t)h & p.mask;
+    const uint32_t s = p.sp & 0xff;
+    const uint64_t mid = h << s;
+    const uint32_t n2 = s ? (uint32_t)(h >> (64 - s)) : 0u;
+    uint32_t r = div21_rem(n2, (uint32_t)(mid >> 32), p.dn, p.v);
+    r = div21_rem(r, (uint32_t)mid, p.dn, p.v);
+    return r >> s;
+}
+
 // ---------------------------------------------------------------------------------
 // HighwayHash (portable form), Redisson flavour.  State lives in 32 VGPRs.
 // ---------------------------------------------------------------------------------

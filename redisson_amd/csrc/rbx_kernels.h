@@ -134,7 +134,7 @@ void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *b
 void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
                                  const uint64_t *seg_off, uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax,
-                                 uint8_t *out, unsigned long long *counts, hipStream_t st);
+                                 uint8_t *out, unsigned long long *counts, hipStream_t st, bool slots);
 void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
 // region-local gathers: 6 loads per lane inside XCD-assigned regions (partitioned-probe roofline)
@@ -145,6 +145,8 @@ void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, u
                          hipStream_t st);
 
 void set_contains_stage1(int v);
+void set_contains_qshape(int v);  // slot kernel (stage 5): P * 10 + Q
+void set_contains_qgrid(int v);
 int get_contains_stage1();
 
 // hll_kernels.hip

@@ -454,7 +454,7 @@ def test_import_dev_many_tenants_parity(client, fresh):
     f.delete()
 
 
-@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5])
 def test_contains_schedules_identical(client, fresh, sched):
     """Every early-exit schedule returns exactly the oracle's per-key answers."""
     from redisson_amd import _lib as L
@@ -475,6 +475,54 @@ def test_contains_schedules_identical(client, fresh, sched):
         cr, pr = ref.contains(*O.fixed_arena(mat), per_key=True)
         assert cg == cr and np.array_equal(pg, pr)
         f.delete()
+
+
+@pytest.mark.parametrize("sched", [4, 5])
+@pytest.mark.parametrize("varlen", [False, True])
+def test_contains_multi_schedules_identical(client, fresh, sched, varlen):
+    """Multi-tenant contains under the staged (4) and per-lane slot (5) kernels: per-key flags and
+    per-tenant counts equal the oracle's, with 1-key, sub-range and multi-range tenant segments."""
+    from redisson_amd import _lib as L
+    from redisson_amd import BloomHandle, bloom_contains_multi
+
+    rng = np.random.default_rng(77 + varlen)
+    shapes = [(14377587, 10), (729, 5), (100003, 17), (4099, 1), (95850583, 7)]
+    seg_lens = [1, 300, 5000, 129, 128, 2, 70000, 1, 257, 3]  # an empty one raises "/ by zero" (:121)
+    names, refs, handles = [], [], []
+    for i in range(len(seg_lens)):
+        size, k = shapes[i % len(shapes)]
+        nm = f"{fresh}-{i}"
+        f = client.getBloomFilter(nm)
+        f.tryInitRaw(size, k)
+        ref = O.OracleBloom(size, k)
+        add = [rng.bytes(int(rng.integers(0, 40)) if varlen else 16) for _ in range(2000)]
+        f.add(Arena(add))
+        ref.add(*O.arena(add))
+        names.append(nm)
+        refs.append((ref, add))
+        handles.append(BloomHandle(client, nm))
+    keys, segs = [], [0]
+    for i, n in enumerate(seg_lens):
+        add = refs[i][1]
+        for _ in range(n):  # half present, half random
+            keys.append(add[int(rng.integers(0, len(add)))] if rng.random() < 0.5 else
+                        rng.bytes(int(rng.integers(0, 40)) if varlen else 16))
+        segs.append(len(keys))
+    segs = np.array(segs, np.uint64)
+    assert L.lib().rbx_tune(b"contains_stage1", sched) == 0
+    try:
+        arena = Arena(keys) if varlen else Arena.fixed(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 16))
+        counts, flags = bloom_contains_multi(client, handles, segs, arena, per_key=True)
+    finally:
+        L.lib().rbx_tune(b"contains_stage1", 4)
+    for s in range(len(seg_lens)):
+        sub = keys[int(segs[s]):int(segs[s + 1])]
+        c, fl = refs[s][0].contains(*O.arena(sub), per_key=True) if sub else (0, np.zeros(0, np.uint8))
+        assert counts[s] == c and np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl)
+    for h in handles:
+        h.close()
+    for nm in names:
+        client.getBloomFilter(nm).delete()
 
 
 @pytest.mark.parametrize("seed", [1, 2])

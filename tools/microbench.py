@@ -228,6 +228,63 @@ def main():
                                   "keys_per_s": m / (med / 1e3), "new": news[mode]}), flush=True)
         L.lib().rbx_tune(b"add_partition", 2)
 
+    if "c3ab" in a.what:
+        # C3 set up once (bench.py run_c3 shape), then contains kernels interleaved round by round
+        # in one process: RBX_C3AB="stage1:shape:grid,..." (shape/grid only used by stage 5)
+        import ctypes as C
+
+        import numpy as np
+
+        nt = int(os.environ.get("RBX_C3_TENANTS", "100000"))
+        pool = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+        rng = np.random.default_rng(0)
+        hs = []
+        for t in range(nt):
+            nm = f"ab:{t:06d}"
+            f = client.getBloomFilter(nm)
+            f.tryInit(1_000_000, 1e-3)
+            nbytes = (f._size + 7) // 8
+            off = int(rng.integers(0, (pool.numel() - nbytes) // 256)) * 256
+            assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), pool.data_ptr() + off, nbytes, sp) == 0
+            hs.append(BloomHandle(client, nm))
+        per = max(1, n // nt)
+        m = per * nt
+        k16 = torch.randint(0, 256, (m, 16), dtype=torch.uint8, device="cuda", generator=g)
+        seg = torch.arange(nt + 1, dtype=torch.int64, device="cuda") * per
+        counts = torch.zeros(nt, dtype=torch.int64, device="cuda")
+        arr = (C.c_void_p * nt)(*[h.h.value for h in hs])
+        dk = device_keys(k16.data_ptr(), m, 16)
+        variants = [tuple(int(x) for x in v.split(":")) for v in
+                    os.environ.get("RBX_C3AB", "4:0:0,5:42:2048,5:22:2048").split(",")]
+
+        def run():
+            assert L.lib().rbx_bloom_contains_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
+                                                         counts.data_ptr(), sp) == 0
+
+        res = {v: [] for v in variants}
+        ref = None
+        for rnd in range(6):
+            for v in variants:
+                L.lib().rbx_tune(b"contains_stage1", v[0])
+                L.lib().rbx_tune(b"contains_multi_slots", 1 if v[0] == 5 else 0)
+                if v[0] == 5:
+                    L.lib().rbx_tune(b"contains_qshape", v[1])
+                    L.lib().rbx_tune(b"contains_qgrid", v[2])
+                counts.zero_()
+                run()
+                c = counts.clone()
+                ref = c if ref is None else ref
+                assert torch.equal(c, ref), v
+                res[v].append(timed(stream, run, 3))
+        L.lib().rbx_tune(b"contains_stage1", 4)
+        L.lib().rbx_tune(b"contains_multi_slots", 2)
+        for v, t in res.items():
+            med = statistics.median(t)
+            print(json.dumps({"bench": "c3ab", "stage1": v[0], "shape": v[1], "grid": v[2], "ms_median": med,
+                              "ms_min": min(t), "ms_max": max(t), "keys_per_s": m / (med / 1e3)}), flush=True)
+        for h in hs:
+            h.close()
+
     if "pflags" in a.what:
         # direct vs partitioned contains, and the partitioned path with its diagnostic switches
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
@@ -264,9 +321,9 @@ def main():
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
         plan = []
         if "stage1" in a.what:
-            plan.append(("C2_2^32", 1 << 32, 7, [0, 1, 2, 4]))
+            plan.append(("C2_2^32", 1 << 32, 7, [0, 1, 2, 4, 5]))
         if "sizes" in a.what:
-            plan += [("C1", 95850583, 7, [1, 4]), ("C3", 14377587, 10, [1, 4]), ("C2_twin", 4294967293, 7, [1, 4])]
+            plan += [("C1", 95850583, 7, [1, 4, 5]), ("C3", 14377587, 10, [1, 4, 5]), ("C2_twin", 4294967293, 7, [1, 4, 5])]
         for name, size, k, s1s in plan:
             fb = client.getBloomFilter("mb-" + name)
             fb.tryInitRaw(size, k)
