@@ -785,3 +785,41 @@ def test_default_partitioned_paths_device_keys(client, fresh):
     assert f.exportBitmap() == ref.redis_string()
     h.close()
     f.delete()
+
+
+def test_multi_filter_table_cache_follows_handles(client, fresh):
+    """Repeated multi-tenant calls reuse the device filter table; a different handle at any
+    position (even one allocated where a closed handle was) or a keyspace change rebuilds it."""
+    from redisson_amd import BloomHandle, bloom_contains_multi
+
+    rng = np.random.default_rng(5)
+    sets = {}
+    for nm, size in (("a", 100003), ("b", 729), ("c", 95850583)):
+        f = client.getBloomFilter(f"{fresh}-{nm}")
+        f.tryInitRaw(size, 7)
+        keys = [rng.bytes(16) for _ in range(3000)]
+        f.add(Arena(keys))
+        ref = O.OracleBloom(size, 7)
+        ref.add(*O.arena(keys))
+        sets[nm] = (ref, keys)
+    probe = sets["a"][1][:1000] + sets["b"][1][:1000] + sets["c"][1][:1000]
+    segs = np.array([0, 1000, 2000, 3000], np.uint64)
+
+    def expect(names):
+        return [sets[n][0].contains(*O.arena(probe[1000 * i:1000 * (i + 1)])) if n else 0
+                for i, n in enumerate(names)]
+
+    ha, hb, hc = (BloomHandle(client, f"{fresh}-{n}") for n in "abc")
+    for _ in range(2):  # the second call takes the cached table
+        assert list(bloom_contains_multi(client, [ha, hb, hc], segs, Arena(probe))) == expect("abc")
+    hb.close()
+    hb2 = BloomHandle(client, f"{fresh}-c")  # may reuse hb's address
+    assert list(bloom_contains_multi(client, [ha, hb2, hc], segs, Arena(probe))) == expect("acc")
+    assert list(bloom_contains_multi(client, [hc, hb2, ha], segs, Arena(probe))) == expect("cca")
+    client.getBloomFilter(f"{fresh}-a").delete()  # keyspace change: the cached table is not reused
+    with pytest.raises(RedisException, match="config has been changed"):  # addConfigCheck (:207-213)
+        bloom_contains_multi(client, [ha, hb2, hc], segs, Arena(probe))
+    for h in (ha, hb2, hc):
+        h.close()
+    for n in "bc":
+        client.getBloomFilter(f"{fresh}-{n}").delete()

@@ -25,7 +25,8 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
          ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
          ("k_stream_probe", r"k_stream_probe<"), ("k_stream_contains", r"k_stream_contains<"),
          ("k_stream_commit", r"k_stream_commit<"),
-         ("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains", r"k_bloom_contains<"),
+         ("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains_q", r"k_bloom_contains_q<"),
+         ("k_bloom_contains", r"k_bloom_contains<"),
          ("k_bloom_add_probe", r"k_bloom_add_probe"), ("k_bloom_add_commit", r"k_bloom_add_commit"),
          ("k_gather_probe", r"k_gather_probe"), ("k_hll_pfadd", r"k_hll_pfadd"), ("k_hll_count", r"k_hll_count"),
          ("k_bitcount", r"k_bitcount")]

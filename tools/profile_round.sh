@@ -21,7 +21,7 @@ python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tc
 # keep summaries only (gpurun copies back <= 64 MiB): stats CSVs, our kernels' counter rows
 for d in pmc_fetch pmc_write pmc_tcc pmc_req; do
   f=$(find "$OUT/$d" -name "*counter_collection.csv" | head -1)
-  [ -n "$f" ] && { head -1 "$f"; grep -E "rbx::" "$f" | head -200; } > "$OUT/${d}_rbx_rows.csv"
+  [ -n "$f" ] && { head -1 "$f"; grep -E "rbx::" "$f" | cat; } > "$OUT/${d}_rbx_rows.csv"
 done
 find "$OUT" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/pmc_req" "$OUT/trace"
