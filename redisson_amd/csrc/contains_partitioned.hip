@@ -42,41 +42,32 @@ __device__ __forceinline__ void bk_direct(unsigned long long e, const uint32_t *
     if ((bm[idx >> 5] & bit_in_word(idx)) == 0u) atomicOr(&miss[key >> 6], 1ULL << (key & 63));
 }
 
-// writes the run s_img[st, st+n) to dst[gb, gb+n); pairs past the capacity are probed directly
-__device__ __forceinline__ void bk_write_run(const unsigned long long *s_img, uint32_t st, uint32_t n, uint64_t gb,
-                                             unsigned long long *__restrict__ dst, uint64_t cap, uint32_t lane,
-                                             const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss) {
-    for (uint32_t t = lane; t < n; t += 64) {
-        const unsigned long long e = s_img[st + t];
-        const uint64_t gp = gb + t;
-        if (gp < cap) __builtin_nontemporal_store(e, dst + gp);
-        else bk_direct(e, bm, miss);
-    }
-}
-
 // Region pairs (emit2 -> probe) are 6 bytes, split into two arrays: lo = offset in the region
 // (19 bits) << 13 | key bits 0-12, hi = key bits 13-26 (chunks hold < 2^27 keys).  Against 8-byte
 // pairs this saves a quarter of emit2's write requests and of the probe's read requests.
 constexpr uint32_t kBkKeyLoBits = 13;
 static_assert(kBkRegionBits + kBkKeyLoBits == 32, "lo word = region offset | low key bits");
 
-__device__ __forceinline__ void bk_write_run6(const unsigned long long *s_img, uint32_t st, uint32_t n, uint64_t gb,
-                                              uint32_t *__restrict__ lo, uint16_t *__restrict__ hi, uint64_t cap,
-                                              uint32_t lane, const uint32_t *__restrict__ bm,
-                                              unsigned long long *__restrict__ miss) {
-    for (uint32_t t = lane; t < n; t += 64) {
-        const unsigned long long e = s_img[st + t];
-        const uint64_t gp = gb + t;
-        if (gp < cap) {
-            const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
-            __builtin_nontemporal_store(((idx & ((1u << kBkRegionBits) - 1)) << kBkKeyLoBits) |
-                                            (key & ((1u << kBkKeyLoBits) - 1)), lo + gp);
-            __builtin_nontemporal_store((uint16_t)(key >> kBkKeyLoBits), hi + gp);
-        } else {
-            bk_direct(e, bm, miss);
-        }
+__device__ __forceinline__ void bk_put6(unsigned long long e, uint64_t gp, uint32_t *__restrict__ lo,
+                                        uint16_t *__restrict__ hi, uint64_t cap, const uint32_t *__restrict__ bm,
+                                        unsigned long long *__restrict__ miss) {
+    if (gp < cap) {
+        const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
+        __builtin_nontemporal_store(((idx & ((1u << kBkRegionBits) - 1)) << kBkKeyLoBits) |
+                                        (key & ((1u << kBkKeyLoBits) - 1)), lo + gp);
+        __builtin_nontemporal_store((uint16_t)(key >> kBkKeyLoBits), hi + gp);
+    } else {
+        bk_direct(e, bm, miss);
     }
 }
+
+// Whole-line runs.  A run written at an arbitrary position touches a partial 64-byte line at
+// each end, and a partial line costs a full write request: at C2 that was ~1/3 of all write
+// requests.  So every reservation is a multiple of the line's entry count (8 pairs of 8 bytes;
+// 32 region pairs = 2 lines of lo words + 1 line of hi halves), the remainder of a run carries
+// in LDS to the block's next tile, and a block's last remainder is padded to a whole line with
+// copies of its last pair (a copy is probed again and sets the same miss bit: no effect).
+constexpr uint32_t kBkLine1 = 8, kBkLine2 = 32;
 
 // K1 -----------------------------------------------------------------------------------
 // Tile = NT * PER keys.  Hash, test bit 0 (one random gather per key), then the survivors'
@@ -95,11 +86,14 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
     constexpr int TILE = NT * PER;
     extern __shared__ __attribute__((aligned(16))) unsigned char bk_lds[];
     unsigned long long *s_img = (unsigned long long *)bk_lds;  // [TILE * (KMAX-1)]
-    uint32_t *s_cnt = (uint32_t *)(s_img + TILE * (KMAX - 1));  // [128]
-    uint32_t *s_start = s_cnt + 128, *s_pos = s_start + 128, *s_gb = s_pos + 128;
+    unsigned long long *s_car = s_img + TILE * (KMAX - 1);      // [128 * kBkLine1] carried pairs
+    uint32_t *s_cnt = (uint32_t *)(s_car + 128 * kBkLine1);      // [128]
+    uint32_t *s_start = s_cnt + 128, *s_pos = s_start + 128, *s_gb = s_pos + 128, *s_full = s_gb + 128,
+             *s_cn = s_full + 128;
     const uint64_t ntiles = (nchunk + TILE - 1) / TILE;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t sub = blockIdx.x % kBkSub;
+    if (threadIdx.x < 128) s_cn[threadIdx.x] = 0;  // visible after the loop's first barrier
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         uint64_t h1[PER], h2[PER];
@@ -147,7 +141,9 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         if (threadIdx.x < 64) bk_scan128(s_cnt, ncoarse, s_start, s_pos);
         else if (threadIdx.x >= 128 && threadIdx.x - 128 < ncoarse) {
             const uint32_t b = threadIdx.x - 128;
-            s_gb[b] = s_cnt[b] ? atomicAdd(&cnt1[b * kBkSub + sub], s_cnt[b]) : 0u;
+            const uint32_t full = (s_cn[b] + s_cnt[b]) & ~(kBkLine1 - 1);
+            s_full[b] = full;
+            s_gb[b] = full ? atomicAdd(&cnt1[b * kBkSub + sub], full) : 0u;
         }
         __syncthreads();
 #pragma unroll
@@ -165,83 +161,140 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         }
         __syncthreads();
         for (uint32_t b = wave; b < ncoarse; b += NT / 64) {
-            const uint32_t n = s_cnt[b];
-            bk_write_run(s_img, s_start[b], n, s_gb[b], pairs1 + (uint64_t)(b * kBkSub + sub) * cap1, cap1, lane, bm,
-                         miss);
+            const uint32_t n = s_cnt[b], cn = s_cn[b], full = s_full[b], st = s_start[b];
+            unsigned long long *dst = pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + s_gb[b];
+            const uint64_t room = cap1 - min<uint64_t>(cap1, s_gb[b]);
+            for (uint32_t t = lane; t < full; t += 64) {  // carried pairs first, then this tile's run
+                const unsigned long long e = t < cn ? s_car[b * kBkLine1 + t] : s_img[st + t - cn];
+                if (t < room) __builtin_nontemporal_store(e, dst + t);
+                else bk_direct(e, bm, miss);
+            }
+            if (full == 0) {  // cn + n < one line: append the run to the carry
+                for (uint32_t t = lane; t < n; t += 64) s_car[b * kBkLine1 + cn + t] = s_img[st + t];
+            } else {          // the remainder is the run's tail (full > cn)
+                for (uint32_t t = lane; t < cn + n - full; t += 64) s_car[b * kBkLine1 + t] = s_img[st + full - cn + t];
+            }
+            if (lane == 0) s_cn[b] = cn + n - full;
         }
         __syncthreads();  // LDS reuse
+    }
+    // the block's last remainders, padded to whole lines
+    for (uint32_t b = wave; b < ncoarse; b += NT / 64) {
+        const uint32_t cn = s_cn[b];
+        if (cn == 0) continue;  // uniform over the wave
+        uint32_t gb = 0;
+        if (lane == 0) gb = atomicAdd(&cnt1[b * kBkSub + sub], kBkLine1);
+        gb = __shfl(gb, 0, 64);
+        if (lane < kBkLine1) {
+            const unsigned long long e = s_car[b * kBkLine1 + min(lane, cn - 1)];
+            if ((uint64_t)gb + lane < cap1)
+                __builtin_nontemporal_store(e, pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + gb + lane);
+            else bk_direct(e, bm, miss);
+        }
     }
 }
 
 // K3 -----------------------------------------------------------------------------------
-// work item = (coarse bucket c, 8192-pair tile); fine bucket = region within c.  Items are
-// numbered c-minor so the blocks running at one time reserve from different buckets' counters.
+// One block per (coarse bucket c, sub-partition) work item, over its 8192-pair tiles in order;
+// fine bucket = region within c.  Items are numbered c-minor so the blocks running at one time
+// reserve from different buckets' region counters.  Runs are whole lines (kBkLine2 pairs), the
+// remainder carries to the next tile (s_car), the item's last remainders are padded.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
                                                   const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
-                                                  uint32_t items_per_c, uint32_t fb, uint32_t nregions, uint64_t cap2,
+                                                  uint32_t fb, uint32_t nregions, uint64_t cap2,
                                                   uint32_t *__restrict__ p2lo, uint16_t *__restrict__ p2hi,
                                                   uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
                                                   uint32_t flags) {
-    constexpr int PER = 8;  // uint4 (two pairs) per thread
-    constexpr int TILE = 16 * NT;
+    constexpr int PER = 4;            // u32x4 (two pairs) per thread
+    constexpr uint32_t TILE = 8 * NT;
     __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
-    __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128];
+    __shared__ unsigned long long s_car[128 * kBkLine2];
+    __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128], s_full[128], s_cn[128];
     const uint32_t nf = 1u << fb, fmask = nf - 1;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t nparts = ncoarse * kBkSub;
-    const uint32_t nitems = nparts * items_per_c;
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        // c-minor: the blocks resident at one time spread over all coarse buckets (and so over
-        // different regions' counters)
-        const uint32_t it = item / nparts, ix = item - it * nparts;
-        const uint32_t c = ix % ncoarse, cs = c * kBkSub + ix / ncoarse;
+    for (uint32_t item = blockIdx.x; item < nparts; item += gridDim.x) {
+        const uint32_t c = item % ncoarse, cs = c * kBkSub + item / ncoarse;
         const uint64_t nc = min<uint64_t>(cnt1[cs], cap1);
-        const uint64_t start = (uint64_t)it * TILE;
-        if (start >= nc) continue;  // uniform over the block
-        const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
-        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
-        __syncthreads();
-        // cap1 and TILE are multiples of 64 pairs: the tile is 16-byte aligned
-        const u32x4 *src = (const u32x4 *)(pairs1 + (uint64_t)cs * cap1 + start);
-        unsigned long long e[2 * PER];
+        if (threadIdx.x < 128) s_cn[threadIdx.x] = 0;
+        // cap1 and TILE are multiples of 64 pairs: every tile is 16-byte aligned
+        const u32x4 *src0 = (const u32x4 *)(pairs1 + (uint64_t)cs * cap1);
+        u32x4 v[PER];  // the next tile, loaded while the current one is bucketed and written
+        auto load = [&](uint64_t st) {
+            const uint32_t mm = (uint32_t)min<uint64_t>(TILE, nc - st);
 #pragma unroll
-        for (int p = 0; p < PER; ++p) {
-            const uint32_t q = 2 * (p * NT + threadIdx.x);
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (q < m) v = __builtin_nontemporal_load(src + p * NT + threadIdx.x);
-            e[2 * p] = w2(v.x, v.y);
-            e[2 * p + 1] = w2(v.z, v.w);
-        }
-#pragma unroll
-        for (int p = 0; p < 2 * PER; ++p) {
-            const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
-            if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) bk_scan128(s_cnt, nf, s_start, s_pos);
-        else if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) {
-            const uint32_t f = threadIdx.x - 128;
-            const uint32_t r = (c << fb) + f;
-            s_gb[f] = (s_cnt[f] && r < nregions) ? atomicAdd(&cnt2[r], s_cnt[f]) : 0u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int p = 0; p < 2 * PER; ++p) {
-            const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
-            if (q < m) {
-                const uint32_t slot = atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
-                s_img[slot] = e[p];
+            for (int p = 0; p < PER; ++p) {
+                v[p] = u32x4{0u, 0u, 0u, 0u};
+                if (2 * (p * NT + threadIdx.x) < mm) v[p] = __builtin_nontemporal_load(src0 + st / 2 + p * NT + threadIdx.x);
             }
+        };
+        if (nc) load(0);
+        for (uint64_t start = 0; start < nc; start += TILE) {
+            const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
+            if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
+            unsigned long long e[2 * PER];
+#pragma unroll
+            for (int p = 0; p < PER; ++p) {
+                e[2 * p] = w2(v[p].x, v[p].y);
+                e[2 * p + 1] = w2(v[p].z, v[p].w);
+            }
+            if (start + TILE < nc) load(start + TILE);
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < 2 * PER; ++p) {
+                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+                if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) bk_scan128(s_cnt, nf, s_start, s_pos);
+            else if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) {
+                const uint32_t f = threadIdx.x - 128;
+                const uint32_t r = (c << fb) + f;
+                const uint32_t full = (s_cn[f] + s_cnt[f]) & ~(kBkLine2 - 1);
+                s_full[f] = full;
+                s_gb[f] = (full && r < nregions) ? atomicAdd(&cnt2[r], full) : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < 2 * PER; ++p) {
+                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+                if (q < m) {
+                    const uint32_t slot = atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
+                    s_img[slot] = e[p];
+                }
+            }
+            __syncthreads();
+            for (uint32_t f = wave; f < nf; f += NT / 64) {
+                const uint32_t n = s_cnt[f], cn = s_cn[f], full = s_full[f], st = s_start[f];
+                const uint64_t rb = (uint64_t)((c << fb) + f) * cap2;
+                for (uint32_t t = lane; t < full; t += 64) {
+                    const unsigned long long v = t < cn ? s_car[f * kBkLine2 + t] : s_img[st + t - cn];
+                    bk_put6(v, (uint64_t)s_gb[f] + t, p2lo + rb, p2hi + rb, cap2, bm, miss);
+                }
+                if (full == 0) {
+                    for (uint32_t t = lane; t < n; t += 64) s_car[f * kBkLine2 + cn + t] = s_img[st + t];
+                } else {
+                    for (uint32_t t = lane; t < cn + n - full; t += 64)
+                        s_car[f * kBkLine2 + t] = s_img[st + full - cn + t];
+                }
+                if (lane == 0) s_cn[f] = cn + n - full;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        for (uint32_t f = wave; f < nf; f += NT / 64) {
-            const uint32_t n = s_cnt[f];
-            const uint64_t rb = (uint64_t)((c << fb) + f) * cap2;
-            bk_write_run6(s_img, s_start[f], n, s_gb[f], p2lo + rb, p2hi + rb, cap2, lane, bm, miss);
+        for (uint32_t f = wave; f < nf; f += NT / 64) {  // the item's last remainders, padded
+            const uint32_t cn = s_cn[f];
+            if (cn == 0) continue;
+            const uint32_t r = (c << fb) + f;
+            uint32_t gb = 0;
+            if (lane == 0) gb = atomicAdd(&cnt2[r], kBkLine2);
+            gb = __shfl(gb, 0, 64);
+            if (lane < kBkLine2)
+                bk_put6(s_car[f * kBkLine2 + min(lane, cn - 1)], (uint64_t)gb + lane, p2lo + (uint64_t)r * cap2,
+                        p2hi + (uint64_t)r * cap2, cap2, bm, miss);
         }
-        __syncthreads();
+        __syncthreads();  // s_cn / s_car reuse by the next item
     }
 }
 
@@ -359,23 +412,22 @@ static void bk_stage1(const PcArgs &a, hipStream_t st) {
     constexpr int TILE = NT1 * bk_per<KMAX>();
     const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
     const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 4096);
-    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 4 * 128 * 4;
+    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 128 * kBkLine1 * 8 + 6 * 128 * 4;
     hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX, NT1>), dim3(g1), dim3(NT1), lds1, st, a.keys, a.base, a.nchunk, a.bm,
                        a.mp, a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
 }
 
 template <int NT2>
 static void bk_emit2(const PcArgs &a, hipStream_t st) {
-    // cap1 is a multiple of 64 pairs and of every tile size used here (>= 16 * 256)
-    const uint32_t items_per_c = (uint32_t)((a.cap1 + 16 * NT2 - 1) / (16 * NT2));
-    hipLaunchKernelGGL((k_bk_emit2<NT2>), dim3(2048), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1, a.ncoarse,
-                       items_per_c, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
+    // one block per (coarse bucket, sub-partition); cap1 is a multiple of the 8 * NT2 tile
+    hipLaunchKernelGGL((k_bk_emit2<NT2>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1,
+                       a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
 }
 
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
     bk_stage1<KLEN, KMAX, 512>(a, st);
-    bk_emit2<512>(a, st);
+    bk_emit2<1024>(a, st);
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
                        a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.flags);
     hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,

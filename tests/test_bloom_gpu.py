@@ -823,3 +823,38 @@ def test_multi_filter_table_cache_follows_handles(client, fresh):
         h.close()
     for n in "bc":
         client.getBloomFilter(f"{fresh}-{n}").delete()
+
+
+def test_partitioned_contains_deterministic_at_c2_scale(client, fresh):
+    """100M keys at C2 geometry: every partitioned call counts exactly what the direct kernel
+    counts (a lost or stray region pair would shift the count by a few keys)."""
+    import torch
+
+    from redisson_amd import _lib as L
+    from redisson_amd import device_keys
+
+    n = 100_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 32, 7)
+    h = BloomHandle(client, fresh)
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    h.add_dev(device_keys(keys.data_ptr(), n // 2, 32), cnt.data_ptr())
+    dk = device_keys(keys.data_ptr(), n, 32)
+    try:
+        L.lib().rbx_tune(b"contains_partition", 0)
+        h.contains_dev(dk, cnt.data_ptr() + 8)
+        L.lib().rbx_tune(b"contains_partition", 1)
+        for i in range(4):
+            h.contains_dev(dk, cnt.data_ptr() + 16 + 8 * i)
+    finally:
+        L.lib().rbx_tune(b"contains_partition", 2)
+    torch.cuda.synchronize()
+    c = cnt.tolist()
+    assert c[1] >= n // 2 and c[2:6] == [c[1]] * 4, c
+    h.close()
+    f.delete()
+    del keys
+    torch.cuda.empty_cache()
