@@ -219,6 +219,9 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
         const uint32_t c = item % ncoarse, cs = c * kBkSub + item / ncoarse;
         const uint64_t nc = min<uint64_t>(cnt1[cs], cap1);
         if (threadIdx.x < 128) s_cn[threadIdx.x] = 0;
+        // an item with no pairs goes straight to the remainder loop, whose waves read the
+        // counters zeroed above by waves 0-1: LDS holds the previous kernel's bytes otherwise
+        __syncthreads();
         // cap1 and TILE are multiples of 64 pairs: every tile is 16-byte aligned
         const u32x4 *src0 = (const u32x4 *)(pairs1 + (uint64_t)cs * cap1);
         u32x4 v[PER];  // the next tile, loaded while the current one is bucketed and written
