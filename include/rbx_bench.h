@@ -17,11 +17,21 @@ int rbx_bench_gather(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, ui
  * region_bytes-sized regions assigned round-robin by blockIdx % 8 (XCD affinity). */
 int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, uint64_t region_bytes,
                              uint64_t nlanes, unsigned grid, void *d_sink, void *stream);
-/* Process-wide tuning knobs (results never change):
- *   "contains_stage1"    early-exit schedule of contains: 0 = all k gathers at once,
- *                        1..3 = that many bits first, 4 = doubling 1,2,4,... (default)
- *   "contains_partition" region-bucketed contains for one large filter: 0 never (default),
- *                        1 always (k in [2,16]), 2 auto (bitmap > 16 MiB and >= 1M keys) */
+/* Process-wide tuning knobs (results never change; A/B runs and tests only):
+ *   "contains_stage1"       early-exit schedule of contains: 0 = all k gathers at once,
+ *                           1..3 = that many bits first, 4 = doubling 1,2,4,... (default),
+ *                           5 = per-lane key slots (one bit per key per round trip)
+ *   "contains_partition"    region-bucketed contains for one large filter: 0 never, 1 always
+ *                           (k in [2,16]), 2 auto (default: bitmap >= 256 MiB, >= 4M keys)
+ *   "contains_partition_flags"  diagnostics of that pipeline: 0 (default), 4, 8, 12
+ *   "add_partition"         region-partitioned add: 0 never, 1 always, 2 auto (default:
+ *                           bitmap >= 8 MiB, >= 1M keys)
+ *   "add_partition_diag"    0 (default) or 4 (diagnostics)
+ *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,
+ *                           2 auto (default: the call's bitmaps exceed 64 MiB)
+ *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44
+ *   "contains_qgrid"        slot kernel grid, 256..8192 (default 2048)
+ *   "stream_contains_slots" ordered-stream contains: 0 staged kernel (default), 1 slot kernel */
 int rbx_tune(const char *key, int value);
 #ifdef __cplusplus
 }

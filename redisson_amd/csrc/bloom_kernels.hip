@@ -592,30 +592,35 @@ __device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx) {
 // adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
 __global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restrict__ op, uint64_t base, uint64_t nchunk,
                                                         uint32_t *__restrict__ adds, uint32_t *__restrict__ nadds) {
-    __shared__ uint32_t s_cnt, s_base;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = (1ULL << lane) - 1;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * 1024; t0 < nchunk; t0 += (uint64_t)gridDim.x * 1024) {
-        if (threadIdx.x == 0) s_cnt = 0;
-        __syncthreads();
-        bool a[4];
-        uint32_t pos[4];
+    // One pass, 4096 commands per block, 16 consecutive per lane: a block scan of the lanes'
+    // add counts and ONE reservation per block.  (A reservation per 1024-command tile, or a
+    // block walking a long slice, left the kernel latency-bound: 79 / 38 us for 6.7M commands.)
+    __shared__ uint32_t s_w[4], s_base;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    uint32_t bits = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t t = t0 + q * 256 + threadIdx.x;
-            a[q] = t < nchunk && op[base + t];
-            const uint64_t mask = __ballot(a[q]);
-            uint32_t wb = 0;
-            if (lane == 0 && mask) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
-            pos[q] = __shfl(wb, 0, 64) + (uint32_t)__popcll(mask & lt);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(nadds, s_cnt) : 0u;
-        __syncthreads();
+    for (int q = 0; q < 16; ++q)
+        if (t0 + q < nchunk && op[base + t0 + q]) bits |= 1u << q;
+    const uint32_t c = (uint32_t)__popc(bits);
+    uint32_t x = c;  // inclusive scan over the wave
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (a[q]) adds[s_base + pos[q]] = (uint32_t)(t0 + q * 256 + threadIdx.x);
-        __syncthreads();
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        s_base = tot ? atomicAdd(nadds, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = s_base + x - c;
+    for (uint32_t w = 0; w < wave; ++w) pos += s_w[w];
+    while (bits) {
+        adds[pos++] = (uint32_t)(t0 + (uint32_t)(__ffs(bits) - 1));
+        bits &= bits - 1;
     }
 }
 
@@ -712,6 +717,146 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
         }
         if (out) out[i] = all;
         present += all;
+    }
+    if (counts) block_add_u64(present, counts);
+}
+
+// The same answers with the per-lane slot schedule of k_bloom_contains_q (§3.1b): one bit per
+// key per round trip, P keys in flight per lane.  A wave's queue holds only the chunk's contains
+// commands (ballot-compacted while the wave hashes a 64*Q-command range), so add commands cost
+// no lane time, and a clear bit consults the prefilter / first-setter table exactly as above.
+template <int KLEN, int P, int Q>
+__global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                           const FilterDesc *__restrict__ filt,
+                                                           const uint32_t *__restrict__ kf,
+                                                           const uint8_t *__restrict__ op,
+                                                           const HTEntry *__restrict__ T, uint32_t log2cap,
+                                                           uint32_t epoch, const uint32_t *__restrict__ prefilter,
+                                                           uint8_t *__restrict__ out,
+                                                           unsigned long long *__restrict__ counts) {
+    constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
+    struct alignas(16) QEnt {
+        uint64_t h1, h2;
+        uint32_t t, fi, idx0, pad;  // chunk-local command index, filter index, first bit
+    };
+    __shared__ QEnt s_q[WAVES][2][RANGE];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t lt = (1ULL << lane) - 1;
+    QEnt *qb = &s_q[wave][0][0];
+    const uint64_t nranges = (nchunk + RANGE - 1) / RANGE;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    uint64_t rnext = (uint64_t)blockIdx.x * WAVES + wave;
+    uint32_t qlen[2] = {0, 0};
+    auto fill = [&](uint32_t b) {  // wave-uniform: the contains of the next non-empty range
+        qlen[b] = 0;
+        while (qlen[b] == 0 && rnext < nranges) {
+            const uint64_t rb = rnext * RANGE;
+#pragma unroll
+            for (uint32_t q = 0; q < Q; ++q) {
+                const uint64_t t = rb + q * 64 + lane;
+                const bool c = t < nchunk && op[base + t] == 0;
+                const uint64_t mask = __ballot(c);
+                if (c) {
+                    QEnt e;
+                    hash_key<KLEN>(keys, base + t, e.h1, e.h2);
+                    e.t = (uint32_t)t;
+                    e.fi = kf[base + t];
+                    e.idx0 = mod63(e.h1 & 0x7fffffffffffffffULL, filt[e.fi].mp);
+                    qb[b * RANGE + qlen[b] + (uint32_t)__popcll(mask & lt)] = e;
+                }
+                qlen[b] += (uint32_t)__popcll(mask);
+            }
+            rnext += nw;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    bool act[P];
+    uint64_t sh1[P], sh2[P], sh[P];
+    uint32_t st[P], sjk[P], sidx[P], sfid[P];  // command index, j | k << 16, bit index, table id
+    const uint32_t *sbm[P];
+    ModC smp[P];
+#pragma unroll
+    for (int s = 0; s < P; ++s) act[s] = false;
+    uint32_t cur = 0, qpos = 0;
+    int stale = -1;
+    fill(0);
+    fill(1);
+    uint64_t present = 0;
+    for (;;) {
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            bool need = !act[s];
+            for (;;) {
+                const uint64_t nm = __ballot(need);
+                if (!nm) break;
+                if (qpos >= qlen[cur]) {
+                    if (stale == (int)(cur ^ 1)) {
+                        fill(cur ^ 1);
+                        stale = -1;
+                    }
+                    if (qlen[cur ^ 1] == 0) break;
+                    stale = (int)cur;
+                    cur ^= 1;
+                    qpos = 0;
+                    continue;
+                }
+                const uint32_t avail = qlen[cur] - qpos;
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
+                if (need && rank < avail) {
+                    const QEnt e = qb[cur * RANGE + qpos + rank];
+                    const FilterDesc f = filt[e.fi];
+                    act[s] = true;
+                    need = false;
+                    sh1[s] = e.h1;
+                    sh2[s] = e.h2;
+                    sh[s] = e.h1 + e.h2;
+                    st[s] = e.t;
+                    sidx[s] = e.idx0;
+                    sbm[s] = f.bm;
+                    smp[s] = mod_compact(f.mp);
+                    sjk[s] = f.k << 16;
+                    sfid[s] = f.fid;
+                }
+                qpos += min<uint32_t>((uint32_t)__popcll(nm), avail);
+            }
+        }
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < P; ++s) any |= act[s];
+        if (!__ballot(any)) break;
+        uint32_t w[P];
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+            if (act[s]) w[s] = sbm[s][sidx[s] >> 5];
+        if (stale >= 0) {
+            fill((uint32_t)stale);
+            stale = -1;
+        }
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            bool fin_p = false;
+            if (act[s]) {
+                bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
+                if (clear) {  // set by an earlier add of this chunk?  Only if the prefilter says so.
+                    const uint32_t pb = prefilter_bit(sfid[s], sidx[s]);
+                    if ((prefilter[pb >> 5] >> (pb & 31)) & 1u)
+                        clear = !(ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s]) < st[s]);
+                }
+                bool fin = clear;
+                if (!clear && ((++sjk[s]) & 0xffffu) >= (sjk[s] >> 16)) {
+                    fin = fin_p = true;
+                } else if (!clear) {
+                    sidx[s] = mod63c(sh[s] & 0x7fffffffffffffffULL, smp[s]);
+                    sh[s] += (sjk[s] & 1) ? sh1[s] : sh2[s];
+                }
+                if (fin) {
+                    act[s] = false;
+                    if (out) out[base + st[s]] = fin_p;
+                }
+            }
+            present += fin_p;
+        }
     }
     if (counts) block_add_u64(present, counts);
 }
@@ -1113,16 +1258,24 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
     }
 }
 
+static int g_stream_slots = 0;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel
+void set_stream_slots(int v) { g_stream_slots = v; }
+
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(a.nchunk, kMaxGrid);
-    const unsigned cgrid = (unsigned)std::min<uint64_t>((a.nchunk + 1023) / 1024, 2048);
+    const unsigned cgrid = (unsigned)((a.nchunk + 4095) / 4096);
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
     hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter);
-    hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out, a.counts);
+    if (g_stream_slots)
+        hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_qgrid)), dim3(256), 0, st, a.keys,
+                           a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out,
+                           a.counts);
+    else
+        hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out, a.counts);
     hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
 }

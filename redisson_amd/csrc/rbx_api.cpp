@@ -2435,6 +2435,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_qshape(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "stream_contains_slots")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_contains_slots in [0, 1]");
+        set_stream_slots(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_qgrid")) {
         if (value < 256 || value > 8192) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qgrid in [256, 8192]");
         set_contains_qgrid(value);

@@ -147,6 +147,7 @@ void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, u
 void set_contains_stage1(int v);
 void set_contains_qshape(int v);  // slot kernel (stage 5): P * 10 + Q
 void set_contains_qgrid(int v);
+void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kernel
 int get_contains_stage1();
 
 // hll_kernels.hip

@@ -525,11 +525,23 @@ def test_contains_multi_schedules_identical(client, fresh, sched, varlen):
         client.getBloomFilter(nm).delete()
 
 
+@pytest.mark.parametrize("slots", [0, 1])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_mixed_stream_in_order_semantics(client, fresh, seed):
+def test_mixed_stream_in_order_semantics(client, fresh, seed, slots):
     """C5 shape: an ordered stream of single-key contains/add commands over tenants with a
     skewed tenant choice; every answer equals the one-after-another oracle replay, including
-    contains right after an add of the same key and adds racing on shared bits."""
+    contains right after an add of the same key and adds racing on shared bits.  Both contains
+    kernels (staged, slots)."""
+    from redisson_amd import _lib as L
+
+    assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
+    try:
+        _stream_case(client, fresh, seed)
+    finally:
+        L.lib().rbx_tune(b"stream_contains_slots", 0)
+
+
+def _stream_case(client, fresh, seed):
     from redisson_amd import bloom_stream
 
     rng = np.random.default_rng(seed)
@@ -566,6 +578,49 @@ def test_mixed_stream_in_order_semantics(client, fresh, seed):
         h.close()
     for n in names:
         client.getBloomFilter(n).delete()
+
+
+def test_mixed_stream_multi_chunk(client, fresh):
+    """A 5M-command stream with k = 32 (chunks of 2^26 / 32 = 2M commands, so three chunks and a
+    multi-block add compaction in each): runs of adds and contains on two filters, replayed on
+    the oracle run by run (filters are independent, and a run of one command type on one filter
+    is exactly one ordered batch)."""
+    from redisson_amd import bloom_stream
+
+    rng = np.random.default_rng(5)
+    shapes = [(50_000_017, 32), (1_000_003, 20)]
+    names = [f"{fresh}-{i}" for i in range(len(shapes))]
+    refs = []
+    for nm, (m, k) in zip(names, shapes):
+        client.getBloomFilter(nm).tryInitRaw(m, k)
+        refs.append(O.OracleBloom(m, k))
+    handles = [BloomHandle(client, nm) for nm in names]
+    n = 5_000_000
+    pool = rng.integers(0, 256, size=(400_000, 16), dtype=np.uint8)
+    keys = pool[rng.integers(0, len(pool), size=n)]
+    kf = np.zeros(n, np.uint32)
+    op = np.zeros(n, np.uint8)
+    runs, i = [], 0
+    while i < n:
+        ln = min(int(rng.integers(1, 40_000)), n - i)
+        f, o = int(rng.integers(0, 2)), int(rng.random() < 0.3)
+        kf[i:i + ln], op[i:i + ln] = f, o
+        runs.append((i, ln, f, o))
+        i += ln
+    out, counts = bloom_stream(client, handles, kf, op, Arena.fixed(keys))
+    want = np.zeros(n, np.uint8)
+    for s, ln, f, o in runs:
+        buf, offs = O.fixed_arena(keys[s:s + ln])
+        _, fl = (refs[f].add if o else refs[f].contains)(buf, offs, per_key=True)
+        want[s:s + ln] = fl
+    assert np.array_equal(out, want)
+    assert counts[0] == int(want[op == 0].sum()) and counts[1] == int(want[op == 1].sum())
+    for nm, r in zip(names, refs):
+        assert client.getBloomFilter(nm).exportBitmap() == r.redis_string()
+    for h in handles:
+        h.close()
+    for nm in names:
+        client.getBloomFilter(nm).delete()
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
