@@ -23,7 +23,8 @@ int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_b
  *                           5 = per-lane key slots (one bit per key per round trip)
  *   "contains_partition"    region-bucketed contains for one large filter: 0 never, 1 always
  *                           (k in [2,16]), 2 auto (default: bitmap >= 256 MiB, >= 4M keys)
- *   "contains_partition_flags"  diagnostics of that pipeline: 0 (default), 4, 8, 12
+ *   "contains_partition_flags"  diagnostics of that pipeline: 0 (default), 4, 8, 12 (wrong
+ *                           answers), 16 (exact: one atomicOr per clear bit, no miss records)
  *   "add_partition"         region-partitioned add: 0 never, 1 always, 2 auto (default:
  *                           bitmap >= 8 MiB, >= 1M keys)
  *   "add_partition_diag"    0 (default) or 4 (diagnostics)

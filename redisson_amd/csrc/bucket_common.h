@@ -42,4 +42,27 @@ __device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uin
     if (2 * lane + 1 < nb) start[2 * lane + 1] = pos[2 * lane + 1] = ex + a;
 }
 
+// the same for nb <= 256 (four buckets per lane)
+__device__ __forceinline__ void bk_scan256(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = 4 * lane + j < nb ? cnt[4 * lane + j] : 0u;
+        s += v[j];
+    }
+    uint32_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    uint32_t ex = x - s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (4 * lane + j < nb) start[4 * lane + j] = pos[4 * lane + j] = ex;
+        ex += v[j];
+    }
+}
+
 }  // namespace rbx

@@ -15,9 +15,10 @@
 //               sub-partitions with their own counters) and written as runs.
 //   K3 emit2  : each coarse bucket's pairs re-bucketed by region (2^FB fine buckets).
 //   K4 probe  : one workgroup per 64 KiB region: region -> LDS, then every pair of the region
-//               tests its bit there; a clear bit sets the key's `miss` bit (rare: only keys that
-//               survived stage 1 by chance).
-//   K5 final  : present = alive AND NOT miss; count (+ per-key bytes).
+//               tests its bit there; a clear bit (only keys that survived stage 1 by chance)
+//               records the key id, bucketed by 2^19-key range.
+//   K5 misses : records -> LDS image of the range's miss words -> OR-ed into `miss`.
+//   K6 final  : present = alive AND NOT miss; count (+ per-key bytes).
 // Measured bound (rocprof PMC, C2): every kernel runs at ~50 G memory requests/s at the L2->EA
 // interface (a read moves 128 B, a write 64 B, an atomic is one request), the same rate the
 // direct kernel's random gathers get; this path issues ~2.8e8 requests per 1e8 keys where the
@@ -302,13 +303,31 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
 }
 
 // K4 -----------------------------------------------------------------------------------
+// A clear bit means the key is absent.  Its key id goes to an LDS record list (one LDS atomic);
+// at the end of the region the list is bucketed by 2^19-key range and written as runs, one
+// reservation per (region, range), for K5 to turn into miss bits.  A scattered 64-bit
+// atomicOr per clear bit (~21M per 1e8 C2 keys: keys that passed bit 0 by chance, ~5.5 clear
+// bits each) cost one memory request each; the runs cost ~1 per 13 records.
+constexpr uint32_t kBkMissBuf = 4096;  // records per region held in LDS; beyond: direct atomicOr
+
+__device__ __forceinline__ void bk_miss_direct(uint32_t key, unsigned long long *miss) {
+    atomicOr(&miss[key >> 6], 1ULL << (key & 63));
+}
+
 __device__ __forceinline__ void bk_test6(const uint32_t *s_bm, uint32_t lo, uint32_t hi, unsigned long long *miss,
-                                         uint32_t flags) {
+                                         uint32_t *s_mrec, uint32_t *s_mn, uint32_t flags) {
     const uint32_t off = lo >> kBkKeyLoBits;
     if ((s_bm[off >> 5] & bit_in_word(off)) == 0u) {  // regions are word-aligned: off's low bits = idx's
         const uint32_t key = (hi << kBkKeyLoBits) | (lo & ((1u << kBkKeyLoBits) - 1));
-        if (flags & 8) miss[0] = 0;  // diagnostics: one fixed store instead of the scattered atomic
-        else atomicOr(&miss[key >> 6], 1ULL << (key & 63));
+        if (flags & 8) {
+            miss[0] = 0;  // diagnostics: one fixed store instead of the miss
+        } else if (flags & 16) {
+            bk_miss_direct(key, miss);  // diagnostics: the direct atomic per clear bit (A/B)
+        } else {
+            const uint32_t slot = atomicAdd(s_mn, 1u);
+            if (slot < kBkMissBuf) s_mrec[slot] = key;
+            else bk_miss_direct(key, miss);
+        }
     }
 }
 
@@ -318,12 +337,18 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ 
                                                    const uint16_t *__restrict__ p2hi,
                                                    const uint32_t *__restrict__ cnt2, uint64_t cap2, uint32_t nregions,
                                                    const uint32_t *__restrict__ bm, uint64_t nwords4,
-                                                   unsigned long long *__restrict__ miss, uint32_t flags) {
+                                                   unsigned long long *__restrict__ miss, uint32_t *__restrict__ mrec,
+                                                   uint32_t *__restrict__ mcnt, uint64_t capm, uint32_t nmranges,
+                                                   uint32_t flags) {
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
+    __shared__ uint32_t s_mrec[kBkMissBuf], s_mimg[kBkMissBuf];
+    __shared__ uint32_t s_mc[256], s_mst[256], s_mpos[256], s_mgb[256], s_mn;
     constexpr uint32_t NT = 1024, G = 6;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
         const uint32_t n = (uint32_t)min<uint64_t>(cnt2[r], cap2);
         if (n == 0) continue;  // uniform
+        if (threadIdx.x == 0) s_mn = 0;  // ordered before the probes by the barrier below
         // region bitmap (nwords4 = bitmap words rounded up to 4; the allocation covers them)
         const uint64_t w0 = (uint64_t)r * kBkRegionWords;
         const uint32_t nv = (uint32_t)min<uint64_t>(kBkRegionWords, nwords4 - w0) / 4;
@@ -360,10 +385,10 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ 
                 const uint32_t q = base + u * NT + threadIdx.x;
                 if (q < n4) {
                     const uint32_t p0 = 4 * q;
-                    bk_test6(s_bm, vl[u].x, vh[u].x & 0xffffu, miss, flags);
-                    if (p0 + 1 < n) bk_test6(s_bm, vl[u].y, vh[u].x >> 16, miss, flags);
-                    if (p0 + 2 < n) bk_test6(s_bm, vl[u].z, vh[u].y & 0xffffu, miss, flags);
-                    if (p0 + 3 < n) bk_test6(s_bm, vl[u].w, vh[u].y >> 16, miss, flags);
+                    bk_test6(s_bm, vl[u].x, vh[u].x & 0xffffu, miss, s_mrec, &s_mn, flags);
+                    if (p0 + 1 < n) bk_test6(s_bm, vl[u].y, vh[u].x >> 16, miss, s_mrec, &s_mn, flags);
+                    if (p0 + 2 < n) bk_test6(s_bm, vl[u].z, vh[u].y & 0xffffu, miss, s_mrec, &s_mn, flags);
+                    if (p0 + 3 < n) bk_test6(s_bm, vl[u].w, vh[u].y >> 16, miss, s_mrec, &s_mn, flags);
                 }
             }
             base += G * NT;
@@ -377,11 +402,81 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ 
                 }
             }
         }
-        __syncthreads();  // s_bm reuse
+        __syncthreads();
+        const uint32_t nm = min(s_mn, kBkMissBuf);
+        if (nm) {  // uniform: bucket the region's miss records by key range
+            if (threadIdx.x < 256) s_mc[threadIdx.x] = 0;
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < nm; i += NT) atomicAdd(&s_mc[s_mrec[i] >> kBkMissRangeBits], 1u);
+            __syncthreads();
+            if (threadIdx.x < 64) bk_scan256(s_mc, nmranges, s_mst, s_mpos);
+            else if (threadIdx.x >= 256 && threadIdx.x - 256 < nmranges) {
+                const uint32_t q = threadIdx.x - 256;
+                s_mgb[q] = s_mc[q] ? atomicAdd(&mcnt[q], s_mc[q]) : 0u;
+            }
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < nm; i += NT) {
+                const uint32_t key = s_mrec[i];
+                s_mimg[atomicAdd(&s_mpos[key >> kBkMissRangeBits], 1u)] = key;
+            }
+            __syncthreads();
+            for (uint32_t q = wave; q < nmranges; q += NT / 64) {
+                const uint32_t cq = s_mc[q], st = s_mst[q];
+                const uint64_t gb = s_mgb[q];
+                for (uint32_t t = lane; t < cq; t += 64) {
+                    const uint32_t key = s_mimg[st + t];
+                    if (gb + t < capm) __builtin_nontemporal_store(key, mrec + (uint64_t)q * capm + gb + t);
+                    else bk_miss_direct(key, miss);
+                }
+            }
+        }
+        __syncthreads();  // s_bm / s_mrec / s_mn reuse
     }
 }
 
 // K5 -----------------------------------------------------------------------------------
+// Miss records -> miss bits.  Item = (key range q, slice of kBkMissSlice records): the slice's
+// key ids set bits of a 64 KiB LDS image of the range's miss words, whose nonzero words are
+// OR-ed into `miss` (consecutive words: one 64-B atomic request per 16 words).  Many small
+// items, not one block per range: one block walking a range's ~1e5 records was latency-bound
+// at ~0.5e9 records/s (0.23 ms at C2).
+constexpr uint32_t kBkMissSlice = 32768;
+
+__global__ __launch_bounds__(1024) void k_bk_misses(const uint32_t *__restrict__ mrec,
+                                                    const uint32_t *__restrict__ mcnt, uint64_t capm,
+                                                    uint32_t nmranges, unsigned long long *__restrict__ miss) {
+    constexpr uint32_t NT = 1024, W = 1u << (kBkMissRangeBits - 5), PER = kBkMissSlice / NT;
+    constexpr uint32_t KM = (1u << kBkMissRangeBits) - 1;
+    __shared__ uint32_t s_m[W];  // 64 KiB
+    const uint32_t nslices = (uint32_t)((capm + kBkMissSlice - 1) / kBkMissSlice);
+    for (uint32_t item = blockIdx.x; item < nmranges * nslices; item += gridDim.x) {
+        const uint32_t q = item % nmranges, sl = item / nmranges;
+        const uint64_t n = min<uint64_t>(mcnt[q], capm), start = (uint64_t)sl * kBkMissSlice;
+        if (start >= n) continue;  // uniform
+        const uint32_t m = (uint32_t)min<uint64_t>(kBkMissSlice, n - start);
+        const uint32_t *src = mrec + (uint64_t)q * capm + start;
+        uint32_t kk[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u) {
+            const uint32_t i = u * NT + threadIdx.x;
+            kk[u] = i < m ? __builtin_nontemporal_load(src + i) : 0xffffffffu;
+        }
+        for (uint32_t w = threadIdx.x; w < W; w += NT) s_m[w] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u)
+            if (kk[u] != 0xffffffffu) atomicOr(&s_m[(kk[u] & KM) >> 5], 1u << (kk[u] & 31));
+        __syncthreads();
+        uint32_t *dst = (uint32_t *)miss + ((uint64_t)q << (kBkMissRangeBits - 5));  // u64 words as LE u32 pairs
+        for (uint32_t w = threadIdx.x; w < W; w += NT) {
+            const uint32_t v = s_m[w];
+            if (v) atomicOr(&dst[w], v);
+        }
+        __syncthreads();  // s_m reuse
+    }
+}
+
+// K6 -----------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bk_final(const unsigned long long *__restrict__ alive,
                                                   const unsigned long long *__restrict__ miss, uint64_t nchunk,
                                                   uint64_t base, uint8_t *__restrict__ out,
@@ -432,7 +527,8 @@ static void bk_chunk(const PcArgs &a, hipStream_t st) {
     bk_stage1<KLEN, KMAX, 512>(a, st);
     bk_emit2<1024>(a, st);
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
-                       a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.flags);
+                       a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges, a.flags);
+    hipLaunchKernelGGL(k_bk_misses, dim3(2048), dim3(1024), 0, st, a.mrec, a.mcnt, a.capm, a.nmranges, a.miss);
     hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,
                        a.out, a.count);
 }

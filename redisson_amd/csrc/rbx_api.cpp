@@ -192,7 +192,7 @@ struct rbx_ctx {
 
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
-    DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2;  // partitioned contains
+    DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits;  // partitioned add
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
@@ -767,7 +767,12 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
     cap1 = (cap1 + 8191) / 8192 * 8192;
     cap2 = (cap2 + 63) / 64 * 64;
     RBX_TRY(c->pc_bits.reserve(ngroups * 16));
-    const uint64_t ncnt = 64 * kBkSub + (uint64_t)nregions;  // cnt1 (padded), cnt2
+    const uint32_t nmranges = (uint32_t)((chunk + (1ULL << kBkMissRangeBits) - 1) >> kBkMissRangeBits);
+    // miss records: sized for 2 per key (C2-like batches hold ~0.2); beyond that the probe falls
+    // back to a direct atomicOr per clear bit, so the answer never depends on the capacity
+    const uint64_t capm = 2ULL << kBkMissRangeBits;
+    RBX_TRY(c->pc_mrec.reserve((uint64_t)nmranges * capm * 4));
+    const uint64_t ncnt = 64 * kBkSub + (uint64_t)nregions + 256;  // cnt1 (padded), cnt2, mcnt
     RBX_TRY(c->pc_cnt.reserve(ncnt * 4));
     RBX_TRY(c->pc_pairs1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
     RBX_TRY(c->pc_pairs2.reserve((uint64_t)nregions * cap2 * 6));  // 6-byte region pairs (lo u32 + hi u16)
@@ -794,6 +799,10 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
         a.pairs1 = c->pc_pairs1.as<unsigned long long>();
         a.p2lo = c->pc_pairs2.as<uint32_t>();
         a.p2hi = (uint16_t *)(a.p2lo + (uint64_t)nregions * cap2);
+        a.mrec = c->pc_mrec.as<uint32_t>();
+        a.mcnt = a.cnt2 + nregions;
+        a.capm = capm;
+        a.nmranges = (uint32_t)((a.nchunk + (1ULL << kBkMissRangeBits) - 1) >> kBkMissRangeBits);
         a.out = d_out;
         a.count = d_count;
         a.flags = (uint32_t)g_partition_flags;
@@ -2406,8 +2415,8 @@ int rbx_tune(const char *key, int value) {
     // DIAGNOSTICS ONLY (tools/microbench.py pflags), results become wrong: 4 = stage 1 emits no
     // pairs, 8 = the probe records no misses.  0 = normal operation.
     if (!strcmp(key, "contains_partition_flags")) {
-        if (value != 0 && value != 4 && value != 8 && value != 12)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12}");
+        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16}");
         g_partition_flags = value;
         return RBX_OK;
     }

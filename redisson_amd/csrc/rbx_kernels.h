@@ -53,6 +53,7 @@ struct AddChunkArgs {
 // partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
 constexpr int kBkRegionBits = 19;  // 2^19 bits = 64 KiB bitmap region = one LDS image
 constexpr uint32_t kBkSub = 16;    // sub-partitions (own counters) per coarse bucket
+constexpr int kBkMissRangeBits = 19;  // probe misses are bucketed by 2^19-key range (64 KiB LDS bitmap)
 struct PcArgs {
     KeysDev keys;
     uint64_t base, nchunk;
@@ -69,6 +70,10 @@ struct PcArgs {
     uint32_t *cnt2;         // nregions, zeroed
     unsigned long long *alive;  // ceil(nchunk/64)
     unsigned long long *miss;   // ceil(nchunk/64), zeroed
+    uint32_t *mrec;         // nmranges * capm: key ids of the probe's clear bits, by 2^19-key range
+    uint32_t *mcnt;         // nmranges, zeroed
+    uint64_t capm;
+    uint32_t nmranges;      // ceil(nchunk / 2^kBkMissRangeBits) <= 256
     unsigned long long *pairs1; // ncoarse * kBkSub * cap1
     uint32_t *p2lo;         // nregions * cap2: region offset << 13 | key bits 0-12
     uint16_t *p2hi;         // nregions * cap2: key bits 13-26

@@ -382,6 +382,36 @@ def test_full_size_2pow32_property(client, fresh):
     f.delete()
 
 
+@pytest.mark.parametrize("flags", [0, 16])
+def test_partitioned_contains_miss_record_overflow(client, fresh, flags):
+    """A half-full filter with k = 16 probed by absent keys: ~3.75 clear bits per key, so the
+    probe's per-region LDS record list (4096) and the per-range record capacity (2 per key)
+    both overflow into the direct atomicOr path; flags 16 takes the direct path for every clear
+    bit.  Per-key answers equal the oracle's either way."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(31)
+    size, k = 1 << 27, 16
+    blob = rng.integers(0, 256, size=size // 8, dtype=np.uint8)
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(size, k)
+    f.importBitmap(blob.tobytes())
+    ref = O.OracleBloom(size, k)
+    ref.bitmap[: size // 8] = blob
+    ref.redis_len = size // 8
+    probe = rng.integers(0, 256, size=(1_500_000, 16), dtype=np.uint8)
+    assert L_.lib().rbx_tune(b"contains_partition", 1) == 0
+    assert L_.lib().rbx_tune(b"contains_partition_flags", flags) == 0
+    try:
+        cg, pg = f.containsEach(Arena.fixed(probe))
+    finally:
+        L_.lib().rbx_tune(b"contains_partition", 2)
+        L_.lib().rbx_tune(b"contains_partition_flags", 0)
+    cr, pr = ref.contains(*O.fixed_arena(probe), per_key=True)
+    assert cg == cr and np.array_equal(pg, pr)
+    f.delete()
+
+
 def test_partitioned_contains_bucket_overflow(client, fresh):
     """Batches that overflow the partitioned path's fixed bucket capacities (a few keys repeated
     hundreds of thousands of times put all pairs into k-1 buckets): the overflowing pairs are
