@@ -12,7 +12,7 @@ N > 1 is launched by torch.distributed.run, one rank per GPU; C2 does not shard
 (weak scaling) and `value` = keys of all ranks / max-over-ranks time.
 
 Printed JSON (rank 0, one line) carries `roofline` for the contains call -- the partitioned
-pipeline k_bk_stage1 -> k_bk_emit2 -> k_bk_probe -> k_bk_final (contains_partitioned.hip),
+pipeline k_bk_stage1 -> k_bk_emit2 -> k_bk_probe -> k_bk_misses -> k_bk_final (contains_partitioned.hip),
 timed with HIP events on the launch stream -- with its PMC traffic and memory-request count
 (profiles/traffic.json, tools/profile_round.sh), an A/B against the direct early-exit kernel,
 and `cpu_baseline`: the oracle's single-thread C restatement timed on a bounded sample.
@@ -298,7 +298,7 @@ def run_c2(args, world, rank, local):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      # one contains call = the partitioned pipeline's kernels in sequence on one stream
-                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<512> + k_bk_probe + k_bk_final",
+                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<1024> + k_bk_probe + k_bk_misses + k_bk_final",
                      "kernel_avg_ms": kern_ms,
                      # the binding limit: memory requests at the L2->EA interface (PMC TCC_EA0_RD/WRREQ),
                      # against the measured random-gather request rate at this working set

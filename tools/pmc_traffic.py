@@ -20,7 +20,7 @@ import os
 import re
 
 SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_bk_probe", r"k_bk_probe"),
-         ("k_bk_final", r"k_bk_final"),
+         ("k_bk_misses", r"k_bk_misses"), ("k_bk_final", r"k_bk_final"), ("k_stream_compact", r"k_stream_compact"),
          ("k_ba_stage1", r"k_ba_stage1<"), ("k_ba_rebucket", r"k_ba_rebucket"), ("k_ba_region", r"k_ba_region"),
          ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
          ("k_stream_probe", r"k_stream_probe<"), ("k_stream_contains", r"k_stream_contains<"),
@@ -88,9 +88,9 @@ def main():
         out[k]["launches_profiled"] = launches.get(k)
     # one API call = these kernels in sequence, possibly once per chunk: per-call totals =
     # all profiled launches' counters / the calls in the profiled run (--calls)
-    for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_final")),
+    for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_misses", "k_bk_final")),
                         ("add_pipeline", ("k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys", "k_ba_final")),
-                        ("stream_pipeline", ("k_stream_probe", "k_stream_contains", "k_stream_commit"))):
+                        ("stream_pipeline", ("k_stream_compact", "k_stream_probe", "k_stream_contains", "k_stream_commit"))):
         if not all(k in out for k in parts) or name not in calls:
             continue
         agg = {"kernels": list(parts), "calls_profiled": calls[name],
