@@ -308,7 +308,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
 // reservation per (region, range), for K5 to turn into miss bits.  A scattered 64-bit
 // atomicOr per clear bit (~21M per 1e8 C2 keys: keys that passed bit 0 by chance, ~5.5 clear
 // bits each) cost one memory request each; the runs cost ~1 per 13 records.
-constexpr uint32_t kBkMissBuf = 4096;  // records per region held in LDS; beyond: direct atomicOr
+constexpr uint32_t kBkMissBuf = 3000;  // records per region held in LDS (C2: ~2.6k); beyond: direct atomicOr
 
 __device__ __forceinline__ void bk_miss_direct(uint32_t key, unsigned long long *miss) {
     atomicOr(&miss[key >> 6], 1ULL << (key & 63));
@@ -333,7 +333,7 @@ __device__ __forceinline__ void bk_test6(const uint32_t *s_bm, uint32_t lo, uint
 
 // One block per region; a lane reads 4 pairs at a time (16 B of lo words + 8 B of hi halves),
 // 6 groups per round trip, the first round issued together with the region's bitmap load.
-__global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ p2lo,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_bk_probe(const uint32_t *__restrict__ p2lo,
                                                    const uint16_t *__restrict__ p2hi,
                                                    const uint32_t *__restrict__ cnt2, uint64_t cap2, uint32_t nregions,
                                                    const uint32_t *__restrict__ bm, uint64_t nwords4,
@@ -341,9 +341,12 @@ __global__ __launch_bounds__(1024) void k_bk_probe(const uint32_t *__restrict__ 
                                                    uint32_t *__restrict__ mcnt, uint64_t capm, uint32_t nmranges,
                                                    uint32_t flags) {
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
-    __shared__ uint32_t s_mrec[kBkMissBuf], s_mimg[kBkMissBuf];
+    // <= 80 KiB so two blocks share a CU: the bucketed image of the miss records reuses the
+    // region bitmap's LDS once the region's probes are done
+    __shared__ uint32_t s_mrec[kBkMissBuf];
+    uint32_t *s_mimg = s_bm;
     __shared__ uint32_t s_mc[256], s_mst[256], s_mpos[256], s_mgb[256], s_mn;
-    constexpr uint32_t NT = 1024, G = 6;
+    constexpr uint32_t NT = 1024, G = 2;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
         const uint32_t n = (uint32_t)min<uint64_t>(cnt2[r], cap2);
