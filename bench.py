@@ -1,27 +1,38 @@
 #!/usr/bin/env python3
-"""bench.py -- Bloom contains throughput on MI355X (BASELINE.json metric, config C2).
+"""bench.py -- Bloom contains throughput on MI355X (BASELINE.json metric, config C2), with the
+C1 / C3 / C4 legs of the same metric family carried in the same JSON line.
 
-Step = one RBloomFilter.contains(Collection) pass (M/RedissonBloomFilter.java:153-186)
-over a batch of 100M synthetic 32-byte keys (50% previously added) against ONE
-2^32-bit filter with k = 7, keys resident in HBM when the timed region starts.
+Step = one RBloomFilter.contains(Collection) pass (M/RedissonBloomFilter.java:153-186) over a
+batch of 100M synthetic 32-byte keys (50% previously added) against ONE 2^32-bit filter with
+k = 7, keys resident in HBM when the timed region starts.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4]
+  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4|c5] [--legs c1,c3,c4|none]
 
-N > 1 is launched by torch.distributed.run, one rank per GPU; C2 does not shard
-("replicas only"), so every rank runs its own replica with its own keys
-(weak scaling) and `value` = keys of all ranks / max-over-ranks time.
+Multi-GPU: one rank per GPU.  The driver launches N > 1 through torch.distributed.run; when
+WORLD_SIZE is unset and --gpus N > 1, bench.py launches those N ranks itself (a child
+torch.distributed.run, started before anything touches the GPU) and exits with its status.
+Every rank asserts WORLD_SIZE == --gpus.
+  - C2 does not shard ("replicas only"): every rank probes its own replica with its
+    own keys (weak scaling); `value` = keys of all ranks / max-over-ranks time.
+  - leg C3 shards 100k tenant filters by CRC16 slot (slot * N / 16384, ClusterConnectionManager
+    .java:814-830) with no data-path collective;
+  - leg C4 partitions PFADD elements over the ranks and merges the 10k x 16384 partial registers
+    with one RCCL uint8 MAX all-reduce (163.84 MB) over xGMI.
+RBX_BENCH_SHARED_GPU=1 rehearses N ranks on one GPU (gloo for the bench's own collectives and
+for the C4 register exchange: RCCL needs a GPU per rank).
 
-Printed JSON (rank 0, one line) carries `roofline` for the contains call -- the partitioned
-pipeline k_bk_stage1 -> k_bk_emit2 -> k_bk_probe -> k_bk_misses -> k_bk_final (contains_partitioned.hip),
-timed with HIP events on the launch stream -- with its PMC traffic and memory-request count
-(profiles/traffic.json, tools/profile_round.sh), an A/B against the direct early-exit kernel,
-and `cpu_baseline`: the oracle's single-thread C restatement timed on a bounded sample.
+Printed JSON (rank 0, one line): `roofline` for the C2 contains call (the partitioned pipeline,
+HIP events on the launch stream), its PMC traffic per access class (profiles/traffic.json from
+tools/profile_round.sh), a streaming-floor roofline of the same call, and `cpu_baseline`: the
+multithreaded C restatement (oracle/rbx_oracle_mt.c) on the host cores on C2 and C1 samples.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,6 +52,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    p.add_argument("--legs", default="c1,c3,c4", help="legs carried in the C2 line: comma list of c1,c3,c4 or 'none'")
+    p.add_argument("--leg-steps", type=int, default=10)
     p.add_argument("--keys", type=int, default=100_000_000, help="keys (C2/C3) or elements (C4) per step per GPU")
     p.add_argument("--tenants", type=int, default=100_000, help="C3 tenant count (whole node)")
     p.add_argument("--elements", type=int, default=1_000_000_000, help="C4 PFADD elements per step per GPU")
@@ -48,11 +61,34 @@ def parse():
     p.add_argument("--tune", default="", help="extra rbx_tune settings for experiments: key=value,key=value")
     p.add_argument("--zipf-s", type=float, default=1.0, help="C5 tenant skew")
     p.add_argument("--add-fraction", type=float, default=0.1, help="C5 share of add commands")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline C2 sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-hostpath", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only (CPU, gloo): every rank reports in, rank 0 prints the rank census")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args()
+
+
+# ------------------------------------------------------------------------------------------
+# ranks
+# ------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks with torch.distributed.run as a CHILD
+    process (nothing in this process has touched the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    log("[bench] launching", " ".join(cmd[2:]))
+    return subprocess.call(cmd)
 
 
 def dist_setup(args):
@@ -61,21 +97,29 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled run")
+        sys.exit(2)
     # RBX_BENCH_SHARED_GPU=1 rehearses the multi-rank flow on a one-GPU box: every rank on
     # cuda:0, gloo for the barrier / max-over-ranks (RCCL cannot put two ranks on one GPU).
     shared = os.environ.get("RBX_BENCH_SHARED_GPU") == "1"
     if shared:
         local = 0
-    torch.cuda.set_device(local)
+    if not args.dry_run:
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if shared:
+        if shared or args.dry_run:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
+
+
+def shared_gpu() -> bool:
+    return os.environ.get("RBX_BENCH_SHARED_GPU") == "1"
 
 
 def barrier(world):
@@ -114,6 +158,21 @@ def sum_over_ranks(world, v: int) -> int:
     return int(t.item())
 
 
+def gather_over_ranks(world, v: int) -> list[int]:
+    if world == 1:
+        return [v]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.zeros(world, dtype=torch.int64, device=_coll_device())
+    t[dist.get_rank()] = v
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]
+
+
+# ------------------------------------------------------------------------------------------
+# measurement helpers
+# ------------------------------------------------------------------------------------------
 def load_traffic(path, kernel, field="hbm_bytes_per_launch"):
     try:
         with open(path) as fh:
@@ -123,9 +182,30 @@ def load_traffic(path, kernel, field="hbm_bytes_per_launch"):
         return None
 
 
+class Timer:
+    """HIP events on the launch stream (torch.cuda.Event records on the stream passed)."""
+
+    def __init__(self, stream):
+        import torch
+
+        self.stream = stream
+        self.e0, self.e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        self.e0.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        import torch
+
+        self.e1.record(self.stream)
+        torch.cuda.synchronize()
+        self.ms = self.e0.elapsed_time(self.e1)
+
+
 def gather_peak(client, nbytes, nkeys, k, stream, gen):
-    """Random 4-byte gathers/s over an nbytes table (k per key, nkeys keys): the request-rate
-    roofline the Bloom kernels are measured against (k_gather_probe, same MLP structure)."""
+    """Uniformly random 4-byte gathers/s over an nbytes table (k per key): the request roofline
+    of a single large filter (k_gather_probe, same MLP structure as the contains kernels)."""
     import torch
 
     from redisson_amd import _lib as L
@@ -135,59 +215,164 @@ def gather_peak(client, nbytes, nkeys, k, stream, gen):
     table = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     table.random_(0, 255, generator=gen)
     L.lib().rbx_bench_gather(client.ctx, table.data_ptr(), nbytes, nkeys, k, sink.data_ptr(), sptr)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(3):
-        L.lib().rbx_bench_gather(client.ctx, table.data_ptr(), nbytes, nkeys, k, sink.data_ptr(), sptr)
-    e1.record(stream)
-    torch.cuda.synchronize()
+    with Timer(stream) as t:
+        for _ in range(3):
+            L.lib().rbx_bench_gather(client.ctx, table.data_ptr(), nbytes, nkeys, k, sink.data_ptr(), sptr)
     del table
-    return nkeys * k / (e0.elapsed_time(e1) / 3 / 1e3)
+    return nkeys * k / (t.ms / 3 / 1e3)
+
+
+def segment_gather_peak(client, table_ptr, table_bytes, seg_bytes, keys_per_seg, nkeys, stream):
+    """Random 4-byte gathers/s with the locality of a multi-tenant batch: consecutive keys share
+    one seg_bytes slice (k_gather_segments, 4 loads per key) -- C3's request roofline."""
+    import torch
+
+    from redisson_amd import _lib as L
+
+    sptr = stream.cuda_stream
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    args = (client.ctx, table_ptr, table_bytes, seg_bytes, keys_per_seg, nkeys, sink.data_ptr(), sptr)
+    L.lib().rbx_bench_gather_segments(*args)
+    with Timer(stream) as t:
+        for _ in range(3):
+            L.lib().rbx_bench_gather_segments(*args)
+    return nkeys * 4 / (t.ms / 3 / 1e3)
+
+
+def stream_read_peak(client, nbytes, stream):
+    """HBM stream-read GB/s (16-byte loads over an nbytes buffer): the PFADD roofline."""
+    import torch
+
+    from redisson_amd import _lib as L
+
+    sptr = stream.cuda_stream
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    L.lib().rbx_bench_stream_read(client.ctx, buf.data_ptr(), nbytes, sink.data_ptr(), sptr)
+    with Timer(stream) as t:
+        for _ in range(5):
+            L.lib().rbx_bench_stream_read(client.ctx, buf.data_ptr(), nbytes, sink.data_ptr(), sptr)
+    del buf
+    return nbytes / (t.ms / 5 / 1e3) / 1e9
 
 
 def request_fields(traffic_json, kernel, ms, peak):
-    """PMC memory requests per launch (TCC_EA0_RDREQ + WRREQ, profiles/traffic.json) vs the peak."""
+    """PMC memory requests per launch (TCC_EA0_RDREQ + WRREQ, profiles/traffic.json) vs a request
+    peak measured at the same working set and locality."""
     reqs = load_traffic(traffic_json, kernel, "requests_per_launch")
     return {"requests_per_launch": reqs, "request_rate_per_s": reqs / (ms / 1e3) if reqs else None,
             "request_peak_per_s": peak, "request_frac": reqs / (ms / 1e3) / peak if reqs and peak else None}
 
 
 # ------------------------------------------------------------------------------------------
-# CPU baseline: oracle restatement (single thread) on a bounded sample of the same workload
+# CPU baseline: the multithreaded C restatement on the host cores (BASELINE.md fallback)
 # ------------------------------------------------------------------------------------------
-def cpu_baseline_c2(target_s: float):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """The host cores this job may use: OMP_NUM_THREADS (16 on the GPU box, its CPU share --
+    os.cpu_count() there reports the whole machine) or else every core."""
+    v = os.environ.get("RBX_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(v)) if v else (os.cpu_count() or 1)
+
+
+def cpu_baseline(target_s: float):
     import numpy as np
 
     from oracle import oracle as O
 
+    T = cpu_threads()
+    # C2 sample: contains of n 32-byte keys (50% present) on a 2^32-bit k = 7 bitmap, repeated
+    # passes until ~target_s of wall time (n bounded to keep host memory small)
     rng = np.random.default_rng(0x5EED0002)
     f = O.OracleBloom(1 << 32, 7)
-    # calibrate on 200k keys
-    cal = rng.integers(0, 256, size=(200_000, 32), dtype=np.uint8)
-    f.add(*O.fixed_arena(cal))
-    t0 = time.perf_counter()
-    f.contains(*O.fixed_arena(cal))
-    per_key = (time.perf_counter() - t0) / cal.shape[0]
-    n = int(min(max(target_s / max(per_key, 1e-9), 200_000), 60_000_000))
+    n = 16_000_000
     added = rng.integers(0, 256, size=(n // 2, 32), dtype=np.uint8)
-    f.add(*O.fixed_arena(added))
+    f.add_mt(*O.fixed_arena(added), nthreads=T)
     probe = np.concatenate([added, rng.integers(0, 256, size=(n - n // 2, 32), dtype=np.uint8)])
+    del added
     b, o = O.fixed_arena(probe)
-    t0 = time.perf_counter()
-    c = f.contains(b, o)
-    dt = time.perf_counter() - t0
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        c = f.contains_mt(b, o, nthreads=T)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s or passes >= 50:
+            break
     assert c >= n // 2
-    return {"value": n / dt, "unit": "keys/s", "cores": 1, "kind": "port",
-            "sample": f"CPU restatement, not reference (Redisson+redis-server absent): oracle/rbx_oracle.c "
-                      f"contains of {n} 32-byte keys (50% present) on a 2^32-bit k=7 bitmap, 1 thread, "
-                      f"{dt:.1f} s"}
+    c2_rate = n * passes / dt
+    del probe, b, o, f
+    # C1: tryInit(1e7, 0.01) -> 95,850,583 bits, k = 7; add 1M 16-byte keys, then contains the
+    # same 1M + 1M fresh (BASELINE.md C1), repeated on fresh bitmaps for >= 3 s
+    size, k = O.bloom_optimal(10_000_000, 0.01)
+    rng = np.random.default_rng(0x5EED0001)
+    keys = rng.integers(0, 256, size=(1_000_000, 16), dtype=np.uint8)
+    probe = np.concatenate([keys, rng.integers(0, 256, size=(1_000_000, 16), dtype=np.uint8)])
+    ka, pa = O.fixed_arena(keys), O.fixed_arena(probe)
+    t_add = t_con = 0.0
+    reps = 0
+    while t_add + t_con < 3.0 or reps < 2:
+        g = O.OracleBloom(size, k)
+        t0 = time.perf_counter()
+        added_new = g.add_mt(*ka, nthreads=T)
+        t1 = time.perf_counter()
+        present = g.contains_mt(*pa, nthreads=T)
+        t2 = time.perf_counter()
+        t_add, t_con, reps = t_add + t1 - t0, t_con + t2 - t1, reps + 1
+    assert present >= 1_000_000 and added_new > 990_000
+    return {"value": c2_rate, "unit": "keys/s", "cores": T, "kind": "port",
+            "sample": f"CPU restatement, not reference (Redisson+redis-server absent): oracle/rbx_oracle_mt.c "
+                      f"contains of {n} 32-byte keys (50% present) on a 2^32-bit k=7 bitmap, {passes} passes, "
+                      f"{T} threads, {dt:.1f} s",
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "c1": {"workload": "tryInit(1e7,0.01) m=95,850,583 k=7: add 1M 16-byte keys, contains 1M present + "
+                               "1M absent", "reps": reps, "threads": T,
+                   "add_keys_per_s": 1_000_000 * reps / t_add, "contains_keys_per_s": 2_000_000 * reps / t_con,
+                   "keys_per_s": 3_000_000 * reps / (t_add + t_con)}}
 
 
 # ------------------------------------------------------------------------------------------
-# C2: single 2^32-bit filter, batch contains of 100M 32-byte keys
+# C2: single 2^32-bit filter, batch contains of 100M 32-byte keys (the headline)
 # ------------------------------------------------------------------------------------------
-def run_c2(args, world, rank, local):
+def host_path_rate(client, name, n=20_000_000):
+    """The rate a Java caller handing over host buffers sees: rbx_bloom_contains on a pinned
+    host arena (keys cross PCIe inside the call)."""
+    import ctypes as C
+
     import numpy as np
+
+    from redisson_amd import _lib as L
+
+    p = C.c_void_p()
+    assert L.lib().rbx_host_alloc(n * 32, C.byref(p)) == 0
+    try:
+        buf = np.ctypeslib.as_array((C.c_uint8 * (n * 32)).from_address(p.value))
+        buf[:] = np.random.default_rng(7).integers(0, 256, size=n * 32, dtype=np.uint8)
+        keys = L.RbxKeys(p.value, None, 32, n)
+        cnt = C.c_uint64()
+        assert L.lib().rbx_bloom_contains(client.ctx, name.encode(), 0, 0, C.byref(keys), None, C.byref(cnt)) == 0
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            assert L.lib().rbx_bloom_contains(client.ctx, name.encode(), 0, 0, C.byref(keys), None,
+                                              C.byref(cnt)) == 0
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        L.lib().rbx_host_free(p)
+    return {"keys_per_s_per_gpu": n / dt, "keys": n, "key_bytes": 32, "pinned": True,
+            "note": "rbx_bloom_contains on a pinned host arena: PCIe-inclusive (what a Java caller handing "
+                    "over off-heap buffers sees); `value` uses HBM-resident keys"}
+
+
+def run_c2(args, world, rank, local):
     import torch
 
     from redisson_amd import BloomHandle, RedissonClient, device_keys
@@ -217,12 +402,8 @@ def run_c2(args, world, rank, local):
 
     # setup: add the first half (timed separately: the "add" half of the metric)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    h.add_dev(device_keys(added.data_ptr(), half, 32), cnt.data_ptr(), stream=sptr)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    add_ms = e0.elapsed_time(e1)
+    with Timer(stream) as t_add:
+        h.add_dev(device_keys(added.data_ptr(), half, 32), cnt.data_ptr(), stream=sptr)
     n_new = int(cnt[0].item())
 
     dk = device_keys(probe.data_ptr(), n, 32)
@@ -231,35 +412,19 @@ def run_c2(args, world, rank, local):
     torch.cuda.synchronize()
     present_one = int(cnt[1].item()) // max(args.warmup, 1) if args.warmup else None
 
-    # random-gather roofline probe at the same working-set size (the 512 MiB bitmap)
-    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
-    bm_table = torch.empty(SIZE // 8, dtype=torch.uint8, device="cuda")
-    bm_table.random_(0, 255, generator=g)
-    L.lib().rbx_bench_gather(client.ctx, bm_table.data_ptr(), SIZE // 8, n, K, sink.data_ptr(), sptr)
-    ge0, ge1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ge0.record(stream)
-    for _ in range(3):
-        L.lib().rbx_bench_gather(client.ctx, bm_table.data_ptr(), SIZE // 8, n, K, sink.data_ptr(), sptr)
-    ge1.record(stream)
-    torch.cuda.synchronize()
-    gather_ms = ge0.elapsed_time(ge1) / 3
-    gathers_per_s = n * K / (gather_ms / 1e3)
-    del bm_table
+    gathers_per_s = gather_peak(client, SIZE // 8, n, K, stream, g)  # same 512 MiB working set
 
     # timed region
     cnt[2].zero_()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        h.contains_dev(dk, cnt.data_ptr() + 16, stream=sptr)
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    with Timer(stream) as t_main:
+        for _ in range(args.steps):
+            h.contains_dev(dk, cnt.data_ptr() + 16, stream=sptr)
     wall = time.perf_counter() - t0
     barrier(world)
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    kern_ms = t_main.ms / args.steps
     total_present = int(cnt[2].item())
     if present_one is not None:
         assert total_present == present_one * args.steps, "contains count changed between steps"
@@ -268,22 +433,22 @@ def run_c2(args, world, rank, local):
     # A/B reference: the same step through the direct early-exit kernel (k_bloom_contains)
     L.lib().rbx_tune(b"contains_partition", 0)
     h.contains_dev(dk, cnt.data_ptr() + 24, stream=sptr)
-    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    d0.record(stream)
-    for _ in range(3):
-        h.contains_dev(dk, cnt.data_ptr() + 24, stream=sptr)
-    d1.record(stream)
-    torch.cuda.synchronize()
+    with Timer(stream) as t_dir:
+        for _ in range(3):
+            h.contains_dev(dk, cnt.data_ptr() + 24, stream=sptr)
     L.lib().rbx_tune(b"contains_partition", 2)
-    direct_ms = d0.elapsed_time(d1) / 3
+    direct_ms = t_dir.ms / 3
     assert int(cnt[3].item()) == 4 * (total_present // args.steps), "direct and partitioned counts differ"
+    hostpath = None if args.no_hostpath or rank != 0 else host_path_rate(client, "bench-c2")
 
     step_s = max_over_ranks(world, max(kern_ms / 1e3, 0.0))
     keys_all = sum_over_ranks(world, n * args.steps)
     value = keys_all / (step_s * args.steps)
     algo_bytes = n * (32 + K * 8)  # 32 B key + k x 8 B gathered per key
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
-    traffic = load_traffic(args.traffic_json, "contains_pipeline")
+    floor_bytes = n * 32 + SIZE // 8  # what any streaming design must move: the keys and the bitmap once
+    traffic = load_traffic(args.traffic_json, "contains_pipeline", "hbm_bytes_by_class") or \
+        load_traffic(args.traffic_json, "contains_pipeline")
     reqs = load_traffic(args.traffic_json, "contains_pipeline", "requests_per_launch")
     res = {
         "metric": "Bloom contains keys/sec (whole node), C2: one 2^32-bit filter, k=7, 32-byte keys",
@@ -298,8 +463,13 @@ def run_c2(args, world, rank, local):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      # one contains call = the partitioned pipeline's kernels in sequence on one stream
-                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<1024> + k_bk_probe + k_bk_misses + k_bk_final",
+                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<1024> + k_bk_probe + "
+                               "k_bk_misses + k_bk_final",
                      "kernel_avg_ms": kern_ms,
+                     # the pipeline's own floor: keys + bitmap streamed once (3.74 GB per call)
+                     "streaming_floor": {"bytes_per_launch": floor_bytes,
+                                         "achieved": floor_bytes / (kern_ms / 1e3) / 1e9,
+                                         "frac": floor_bytes / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
                      # the binding limit: memory requests at the L2->EA interface (PMC TCC_EA0_RD/WRREQ),
                      # against the measured random-gather request rate at this working set
                      "requests_per_launch": reqs,
@@ -309,24 +479,76 @@ def run_c2(args, world, rank, local):
                      # north-star definition: keys/s x k / measured random-gather peak at this
                      # working set (> 1: early exit and LDS probes avoid most random gathers)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
-        "extra": {"add_keys_per_s_per_gpu": half / (add_ms / 1e3), "add_new_keys": n_new,
+        "extra": {"add_keys_per_s_per_gpu": half / (t_add.ms / 1e3), "add_new_keys": n_new,
                   "present_per_step": total_present // args.steps, "wall_s_timed": wall,
                   "contains_direct_kernel_ms": direct_ms,
                   "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3),
                   # the setup add = the partitioned add pipeline (add_partitioned.hip), PMC per call
-                  "add_ms": add_ms,
-                  "add_traffic": load_traffic(args.traffic_json, "add_pipeline"),
-                  "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch")},
+                  "add_ms": t_add.ms,
+                  "add_traffic": load_traffic(args.traffic_json, "add_pipeline", "hbm_bytes_by_class") or
+                  load_traffic(args.traffic_json, "add_pipeline"),
+                  "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch"),
+                  "host_path": hostpath},
     }
     h.close()
+    f.delete()
     client.shutdown()
+    del added, probe
+    torch.cuda.empty_cache()
     return res
+
+
+# ------------------------------------------------------------------------------------------
+# C1 leg: tryInit(1e7, 0.01), add 1M 16-byte keys, contains 1M present + 1M absent
+# ------------------------------------------------------------------------------------------
+def run_c1(args, world, rank, local):
+    import torch
+
+    from redisson_amd import BloomHandle, RedissonClient, device_keys
+
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+    client = RedissonClient(local)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0001 + 1000 * rank)
+    keys = torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+    probe = torch.cat([keys, torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)])
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    t_add = t_con = 0.0
+    reps = max(2, args.leg_steps)
+    for r in range(args.warmup + reps):  # a fresh filter per rep: add() sees the empty bitmap every time
+        name = f"bench-c1-{r}"
+        f = client.getBloomFilter(name)
+        assert f.tryInit(10_000_000, 0.01)
+        h = BloomHandle(client, name)
+        cnt.zero_()
+        torch.cuda.synchronize()
+        with Timer(stream) as ta:
+            h.add_dev(device_keys(keys.data_ptr(), 1_000_000, 16), cnt.data_ptr(), stream=sptr)
+        with Timer(stream) as tc:
+            h.contains_dev(device_keys(probe.data_ptr(), 2_000_000, 16), cnt.data_ptr() + 8, stream=sptr)
+        if r >= args.warmup:
+            t_add, t_con = t_add + ta.ms, t_con + tc.ms
+        added, present = cnt.tolist()
+        assert added > 990_000 and present >= 1_000_000
+        h.close()
+        f.delete()
+    client.shutdown()
+    add_s = max_over_ranks(world, t_add / reps / 1e3)
+    con_s = max_over_ranks(world, t_con / reps / 1e3)
+    return {"metric": "C1 Bloom add+contains keys/sec (whole node)", "unit": "keys/s",
+            "value": 3_000_000 * world / (add_s + con_s), "reps": reps,
+            "add_keys_per_s": 1_000_000 * world / add_s, "contains_keys_per_s": 2_000_000 * world / con_s,
+            "add_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "size_bits": 95_850_583, "k": 7,
+            "config": "tryInit(1e7,0.01): add 1M 16-byte keys, contains 1M present + 1M absent, keys in HBM, "
+                      "per GPU (replicas)"}
 
 
 # ------------------------------------------------------------------------------------------
 # C3: 100k tenant filters tryInit(1e6, 1e-3), sharded by CRC16 slot across the node's GPUs
 # ------------------------------------------------------------------------------------------
-def run_c3(args, world, rank, local):
+def run_c3(args, world, rank, local, steps, warmup):
     import ctypes as C
 
     import numpy as np
@@ -372,21 +594,23 @@ def run_c3(args, world, rank, local):
         assert L.lib().rbx_bloom_contains_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
                                                      counts.data_ptr(), sptr) == 0
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     barrier(world)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
+    with Timer(stream) as t:
+        for _ in range(steps):
+            step()
+    ms = t.ms / steps
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
-    present = int(counts.sum().item()) / max(args.warmup + args.steps, 1)
-    peak = gather_peak(client, 4 << 30, n, 4, stream, g)  # random gathers over a table far past the caches
+    per_rank_tenants = gather_over_ranks(world, nt)
+    present = int(counts.sum().item()) / max(warmup + steps, 1)
+    del pool
+    # request roofline at C3's locality: `per` consecutive keys gather inside one 1.8 MB slice
+    tbl = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
+    peak = segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), (size + 7) // 8, per, n, stream)
+    del tbl
     algo = n * (16 + k * 8)
     achieved = algo / (ms / 1e3) / 1e9
     # 180 GB of bitmaps: the slot kernel unless a staged schedule was forced
@@ -395,21 +619,28 @@ def run_c3(args, world, rank, local):
     kdesc = "k_bloom_contains_q<16,true,2,2>" if slots else f"k_bloom_contains_multi<16,16,{args.stage1}>"
     res = {
         "metric": "Bloom contains keys/sec (whole node), C3: 100k tenant filters tryInit(1e6,1e-3), CRC16-slot sharded",
-        "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": value, "unit": "keys/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"C3 one contains(Collection) per tenant, {per} random 16-byte keys each, "
                                f"{nt} of {NT} tenants on this GPU (slot*N/16384), filters at design fill 0.5",
-                   "tenants_total": NT, "tenants_this_gpu": nt, "size_bits": size, "k": k, "keys_per_gpu": n,
+                   "tenants_total": NT, "tenants_this_gpu": nt, "tenants_per_rank": per_rank_tenants,
+                   "size_bits": size, "k": k, "keys_per_gpu": n,
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, kname),
-                     "kernel": kdesc, "kernel_avg_ms": ms, **request_fields(args.traffic_json, kname, ms, peak)},
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.traffic_json, kname, "hbm_bytes_by_class") or
+                     load_traffic(args.traffic_json, kname),
+                     "kernel": kdesc, "kernel_avg_ms": ms,
+                     "request_peak_kind": "k_gather_segments: 4 random loads per key inside its tenant's slice",
+                     **request_fields(args.traffic_json, kname, ms, peak)},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
     for h in handles:
         h.close()
     client.shutdown()
+    del keys
+    torch.cuda.empty_cache()
     return res
 
 
@@ -466,17 +697,18 @@ def run_c5(args, world, rank, local):
         step()
     torch.cuda.synchronize()
     barrier(world)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
+    with Timer(stream) as t:
+        for _ in range(args.steps):
+            step()
+    ms = t.ms / args.steps
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
     top = int(torch.bincount(kf.long(), minlength=nt).max().item())
-    peak = gather_peak(client, 4 << 30, n, 4, stream, g)
+    del pool
+    tbl = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
+    peak = segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), 1_797_199, 1, n, stream)
+    del tbl
+    algo = n * (64 + 10 * 8)
     res = {
         "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
         "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -487,10 +719,13 @@ def run_c5(args, world, rank, local):
                                "64-byte keys, in-order semantics",
                    "tenants_this_gpu": nt, "ops_per_gpu": n, "hottest_tenant_ops": top,
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
-        "roofline": {"bound": "hbm", "achieved": n * (64 + 10 * 8) / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": n * (64 + 10 * 8) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": load_traffic(args.traffic_json, "stream_pipeline"),
+        "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.traffic_json, "stream_pipeline", "hbm_bytes_by_class") or
+                     load_traffic(args.traffic_json, "stream_pipeline"),
                      "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms,
+                     "request_peak_kind": "k_gather_segments, one key per tenant slice (uniform tenants: "
+                                          "no Zipf reuse, a lower bound on C5's locality)",
                      **request_fields(args.traffic_json, "stream_pipeline", ms, peak)},
     }
     for h in handles:
@@ -502,7 +737,7 @@ def run_c5(args, world, rank, local):
 # ------------------------------------------------------------------------------------------
 # C4: 10k HLLs, PFADD of 16-byte elements, PFCOUNT of all, RCCL max merge
 # ------------------------------------------------------------------------------------------
-def run_c4(args, world, rank, local):
+def run_c4(args, world, rank, local, steps, warmup):
     import ctypes as C
 
     import numpy as np
@@ -512,7 +747,7 @@ def run_c4(args, world, rank, local):
     from redisson_amd import _lib as L
 
     NH = 10_000
-    per = max(1, args.elements // NH)  # elements per HLL per GPU per step
+    per = max(1, args.elements // NH)  # elements per HLL per GPU per step (this rank's partition)
     n = NH * per
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -530,22 +765,24 @@ def run_c4(args, world, rank, local):
     el = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
     changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
     dk = device_keys(el.data_ptr(), n, 16)
-    for _ in range(args.warmup):
+
+    def step():
         assert L.lib().rbx_hll_add_multi_dev(client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk),
                                              changed.data_ptr(), sptr) == 0
+
+    for _ in range(warmup):
+        step()
     torch.cuda.synchronize()
     barrier(world)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.steps):
-        assert L.lib().rbx_hll_add_multi_dev(client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk),
-                                             changed.data_ptr(), sptr) == 0
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
-    merge_ms = None
-    if world > 1 and os.environ.get("RBX_BENCH_SHARED_GPU") != "1":
-        # element-partitioned registers -> RCCL uint8 max all-reduce over xGMI
+    with Timer(stream) as t:
+        for _ in range(steps):
+            step()
+    ms = t.ms / steps
+    del el
+    nbytes = NH * 16384
+    merge = {"allreduce_bytes": nbytes, "nranks_rccl": None, "rccl_max_allreduce_ms": None}
+    if world > 1 and not shared_gpu():
+        # element-partitioned registers -> ONE RCCL uint8 max all-reduce over xGMI
         import torch.distributed as dist
 
         uid = (C.c_uint8 * 128)()
@@ -554,42 +791,75 @@ def run_c4(args, world, rank, local):
         obj = [bytes(uid)]
         dist.broadcast_object_list(obj, src=0)
         uid = (C.c_uint8 * 128).from_buffer_copy(obj[0])
-        assert L.lib().rbx_rccl_init(client.ctx, uid, world, rank) == 0
+        assert L.lib().rbx_rccl_init(client.ctx, uid, world, rank) == 0, L.last_error()
+        nr, rk = C.c_int(), C.c_int()
+        assert L.lib().rbx_rccl_info(client.ctx, C.byref(nr), C.byref(rk)) == 0
         assert L.lib().rbx_hll_allreduce_max(client.ctx, arr, NH) == 0  # warm
         L.lib().rbx_synchronize(client.ctx)
+        times = []
+        for _ in range(3):
+            barrier(world)
+            t0 = time.perf_counter()
+            assert L.lib().rbx_hll_allreduce_max(client.ctx, arr, NH) == 0
+            L.lib().rbx_synchronize(client.ctx)
+            times.append(time.perf_counter() - t0)
+        mt = max_over_ranks(world, min(times))
+        algbw = nbytes / mt / 1e9
+        merge.update({"exchange": "RCCL ncclAllReduce(ncclUint8, ncclMax), pack -> all-reduce -> unpack_max",
+                      "nranks_rccl": nr.value, "rccl_max_allreduce_ms": mt * 1e3,
+                      "algbw_GBps": algbw, "busbw_GBps": algbw * 2 * (world - 1) / world})
+    elif world > 1:
+        # shared-GPU rehearsal: the same pack / unpack_max exchange, the all-reduce over gloo
+        import torch.distributed as dist
+
+        buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
         barrier(world)
         t0 = time.perf_counter()
-        assert L.lib().rbx_hll_allreduce_max(client.ctx, arr, NH) == 0
-        L.lib().rbx_synchronize(client.ctx)
-        merge_ms = (time.perf_counter() - t0) * 1e3
+        assert L.lib().rbx_hll_pack_registers(client.ctx, arr, NH, buf.data_ptr(), sptr) == 0
+        torch.cuda.synchronize()
+        host = buf.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.MAX)
+        buf.copy_(host.cuda())
+        assert L.lib().rbx_hll_unpack_max_registers(client.ctx, arr, NH, buf.data_ptr(), sptr) == 0
+        torch.cuda.synchronize()
+        mt = max_over_ranks(world, time.perf_counter() - t0)
+        merge.update({"exchange": "gloo (shared-GPU rehearsal: RCCL needs one GPU per rank)",
+                      "exchange_ms": mt * 1e3})
     out = np.zeros(NH, np.uint64)
     t0 = time.perf_counter()
     assert L.lib().rbx_hll_count_each_handles(client.ctx, arr, NH, out.ctypes.data_as(L.u64p)) == 0
     count_ms = (time.perf_counter() - t0) * 1e3
+    peak_gbs = stream_read_peak(client, 8 << 30, stream)
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
     achieved = n * 16 / (ms / 1e3) / 1e9
     res = {
         "metric": "HLL PFADD elems/sec (whole node), C4: 10k HLLs, 16-byte elements",
-        "value": value, "unit": "elems/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": value, "unit": "elems/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"C4 PFADD {per} x 16-byte elements into each of 10k HLLs per GPU",
                    "elements_per_gpu": n, "parallelism": f"element-partitioned x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.traffic_json, "k_hll_pfadd"),
-                     "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms},
-        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean()), "rccl_max_allreduce_ms": merge_ms,
-                  "allreduce_bytes": NH * 16384},
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.traffic_json, "k_hll_pfadd", "hbm_bytes_by_class") or
+                     load_traffic(args.traffic_json, "k_hll_pfadd"),
+                     "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms,
+                     # elems/s x 16 B / the measured HBM stream-read peak
+                     "stream_read_peak_GBps": peak_gbs, "stream_frac": achieved / peak_gbs},
+        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean()), "merge": merge},
     }
     for hp in hs:
         L.lib().rbx_hll_close(hp)
     client.shutdown()
+    torch.cuda.empty_cache()
     return res
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     world, rank, local = dist_setup(args)
     if args.stage1 is not None:
         from redisson_amd import _lib as L
@@ -603,16 +873,38 @@ def main():
         key, val = kv.split("=")
         assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
     log(f"[bench] rank {rank}/{world} workload {args.workload}")
+    if args.dry_run:
+        census = gather_over_ranks(world, os.getpid())
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": len(census), "pids": census}), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+        return
     if args.workload == "c2":
         res = run_c2(args, world, rank, local)
+        legs = [] if args.legs == "none" else [x for x in args.legs.split(",") if x]
+        ls, lw = min(args.steps, args.leg_steps), min(args.warmup, 2)
+        res["legs"] = {}
+        for leg in legs:
+            log(f"[bench] rank {rank} leg {leg}")
+            if leg == "c1":
+                res["legs"]["c1"] = run_c1(args, world, rank, local)
+            elif leg == "c3":
+                res["legs"]["c3"] = run_c3(args, world, rank, local, ls, lw)
+            elif leg == "c4":
+                res["legs"]["c4"] = run_c4(args, world, rank, local, ls, lw)
+            else:
+                raise SystemExit(f"unknown leg {leg}")
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline_c2(args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     elif args.workload == "c4":
-        res = run_c4(args, world, rank, local)
+        res = run_c4(args, world, rank, local, args.steps, args.warmup)
     elif args.workload == "c5":
         res = run_c5(args, world, rank, local)
     else:
-        res = run_c3(args, world, rank, local)
+        res = run_c3(args, world, rank, local, args.steps, args.warmup)
     if rank == 0:
         res.setdefault("cpu_baseline", None)
         print(json.dumps(res), flush=True)

@@ -15,7 +15,8 @@
  *    M/RedissonObject.java:319-321).  The engine is codec-agnostic.
  *  - A context owns one GPU.  Calls on one context are serialized (a batch is the
  *    unit of serialization, matching the reference's pipeline order); calls from
- *    several threads are safe.
+ *    several threads are safe.  Handles keep their context's memory alive: closing a
+ *    handle after rbx_shutdown is safe, any other call on it returns RBX_E_ILLEGAL_STATE.
  *  - *_dev variants take DEVICE pointers and a hipStream_t (as void*; NULL = the
  *    context's stream), enqueue work and return without synchronizing.  Counts are
  *    accumulated into device-resident unsigned long long words.  Per-call device scratch
@@ -43,7 +44,9 @@ enum {
     RBX_E_WRONGTYPE = -5,        /* RedisException WRONGTYPE / INVALIDOBJ            */
     RBX_E_DEVICE = -6,           /* HIP / RCCL runtime failure                       */
     RBX_E_OOM = -7,              /* device or host allocation failure                */
-    RBX_E_NO_SUCH_KEY = -8       /* RedisException "ERR no such key" (RENAME)        */
+    RBX_E_NO_SUCH_KEY = -8,      /* RedisException "ERR no such key" (RENAME)        */
+    RBX_E_REDIS = -9             /* other RedisException replies, e.g. "ERR bit offset is not an
+                                    integer or out of range" (a negative-size filter past 2^32 bits) */
 };
 
 typedef struct rbx_ctx rbx_ctx;
@@ -59,9 +62,18 @@ typedef struct rbx_keys {
     uint64_t n;
 } rbx_keys;
 
+/* A key name of any bytes (Redis keys are binary-safe; Spring Data passes byte[] keys,
+ * redisson-spring-data-32 RedissonConnection.java:2203).  The *_n entry points take these; the
+ * others take NUL-terminated names. */
+typedef struct rbx_name {
+    const uint8_t *bytes;
+    uint64_t len;
+} rbx_name;
+
 /* The {name}:config hash (M/RedissonBloomFilter.java:285-288). */
 typedef struct rbx_bloom_config {
-    uint64_t size;               /* "size" (bits)                           */
+    int64_t size;                /* "size" (bits; Java long: tryInit with a negative
+                                    expectedInsertions stores a negative size, :270-276) */
     uint32_t hash_iterations;    /* "hashIterations" (k)                    */
     int64_t expected_insertions; /* "expectedInsertions" (0 if raw-created) */
     double false_probability;    /* "falseProbability"                      */
@@ -96,7 +108,7 @@ int rbx_slot_to_gpu(int slot, int n_gpus);
 
 /* ---- Bloom sizing: RedissonBloomFilter.optimalNumOfBits/HashFunctions :79-88 ---- */
 int rbx_bloom_optimal_config(int64_t expected_insertions, double false_probability,
-                             uint64_t *size_out, uint32_t *k_out);
+                             int64_t *size_out, uint32_t *k_out);
 
 /* ---- RBloomFilter (by name) -- M/api/RBloomFilter.java:27-113 ---------------------- */
 /* tryInit(expectedInsertions, falseProbability)  M/RedissonBloomFilter.java:262-300 */
@@ -107,9 +119,10 @@ int rbx_bloom_try_init(rbx_ctx *ctx, const char *name, int64_t expected_insertio
 int rbx_bloom_init_raw(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k, int *created);
 /* readConfig() HGETALL {name}:config  :240-255 (RBX_E_ILLEGAL_STATE if absent) */
 int rbx_bloom_read_config(rbx_ctx *ctx, const char *name, rbx_bloom_config *out);
-/* add(Collection) :104-137.  size/k are the caller's cached config, checked like
- * addConfigCheck :207-213.  out_new (nullable): 1 byte per key, 1 iff the key
- * counts as newly added under the reference's in-order SETBIT semantics. */
+/* add(Collection) :104-137.  size/k are the caller's cached config (size = the Java long's
+ * bits; 0 = read the config first, :106-108), checked like addConfigCheck :207-213.
+ * out_new (nullable): 1 byte per key, 1 iff the key counts as newly added under the
+ * reference's in-order SETBIT semantics. */
 int rbx_bloom_add(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k,
                   const rbx_keys *keys, uint8_t *out_new, uint64_t *out_count);
 /* contains(Collection) :153-186.  out_present (nullable): 1 byte per key. */
@@ -117,6 +130,19 @@ int rbx_bloom_contains(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k
                        const rbx_keys *keys, uint8_t *out_present, uint64_t *out_count);
 /* count() :215-227 (BITCOUNT + the host double formula) */
 int rbx_bloom_count(rbx_ctx *ctx, const char *name, int64_t *out);
+/* the same four with binary names */
+int rbx_bloom_try_init_n(rbx_ctx *ctx, rbx_name name, int64_t expected_insertions, double false_probability,
+                         int *created);
+int rbx_bloom_read_config_n(rbx_ctx *ctx, rbx_name name, rbx_bloom_config *out);
+int rbx_bloom_add_n(rbx_ctx *ctx, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                    uint8_t *out_new, uint64_t *out_count);
+int rbx_bloom_contains_n(rbx_ctx *ctx, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                         uint8_t *out_present, uint64_t *out_count);
+int rbx_bloom_count_n(rbx_ctx *ctx, rbx_name name, int64_t *out);
+/* DEL k1..kn (*deleted = keys removed) and EXISTS k1..kn (*count = existing keys, repeats
+ * counted) over keys of any type -- RObject.delete / isExists for any name */
+int rbx_del_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, int *deleted);
+int rbx_exists_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, int *count);
 /* BITCOUNT name */
 int rbx_bloom_bitcount(rbx_ctx *ctx, const char *name, uint64_t *out);
 /* delete() :230-232 -- DEL name {name}:config; *deleted = number of keys removed */
@@ -136,6 +162,8 @@ int rbx_bloom_renamenx(rbx_ctx *ctx, const char *name, const char *new_name, int
  * RHyperLogLog {name}. */
 int rbx_pexpire(rbx_ctx *ctx, const char *const *names, uint32_t n, int64_t when_ms, int absolute, int cond,
                 int *result);
+int rbx_pexpire_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, int64_t when_ms, int absolute, int cond,
+                  int *result);
 /* clearExpireAsync (:241-251): PERSIST every key, *result = 1 iff any timeout was removed */
 int rbx_persist(rbx_ctx *ctx, const char *const *names, uint32_t n, int *result);
 /* remainTimeToLiveAsync (:193-195) = PTTL, getExpireTimeAsync (:203-205) = PEXPIRETIME of one key:
@@ -153,6 +181,7 @@ int rbx_bloom_import_dev(rbx_ctx *ctx, const char *name, const uint8_t *d_bytes,
 
 /* ---- Bloom handles and the device-resident batch path ------------------------------ */
 int rbx_bloom_open(rbx_ctx *ctx, const char *name, rbx_bloom **out);
+int rbx_bloom_open_n(rbx_ctx *ctx, rbx_name name, rbx_bloom **out);
 int rbx_bloom_close(rbx_bloom *b);
 int rbx_bloom_handle_config(const rbx_bloom *b, uint64_t *size, uint32_t *k);
 /* contains over device-resident keys; *d_count += present keys (device word). */
@@ -220,10 +249,19 @@ int rbx_hll_export_enc(rbx_ctx *ctx, const char *name, int encoding, uint8_t *ou
 int rbx_hll_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint64_t len);
 int rbx_hll_delete(rbx_ctx *ctx, const char *name, int *deleted);
 int rbx_hll_exists(rbx_ctx *ctx, const char *name, int *exists);
+/* binary-name forms (Spring Data pfAdd/pfCount/pfMerge with byte[] keys,
+ * redisson-spring-data-32 RedissonConnection.java:2200-2226) */
+int rbx_hll_add_multi_n(rbx_ctx *ctx, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                        const rbx_keys *elements, uint8_t *out_changed);
+int rbx_hll_count_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, uint64_t *out);
+int rbx_hll_merge_n(rbx_ctx *ctx, rbx_name dest, const rbx_name *srcs, uint32_t nsrc);
+int rbx_hll_export_enc_n(rbx_ctx *ctx, rbx_name name, int encoding, uint8_t *out, uint64_t cap, uint64_t *len);
+int rbx_hll_import_n(rbx_ctx *ctx, rbx_name name, const uint8_t *bytes, uint64_t len);
 
 /* ---- HLL handles and the device-resident path ------------------------------------- */
 /* Opens (creating an empty HLL if absent and create != 0). */
 int rbx_hll_open(rbx_ctx *ctx, const char *name, int create, rbx_hll **out);
+int rbx_hll_open_n(rbx_ctx *ctx, rbx_name name, int create, rbx_hll **out);
 int rbx_hll_close(rbx_hll *h);
 /* Device address of the 16384 u8 registers (raw, one byte per register). */
 int rbx_hll_registers_dev(rbx_hll *h, void **d_regs);
@@ -235,12 +273,23 @@ int rbx_hll_add_multi_dev(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t nseg,
 /* Single-key PFCOUNT of each handle into host out[i] (synchronous). */
 int rbx_hll_count_each_handles(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n, uint64_t *out);
 
+/* Register exchange of an element-partitioned HLL set (any transport): pack copies the
+ * registers of hlls[i] to d_buf[i*16384 .. (i+1)*16384) in the caller's order; unpack_max
+ * merges them back (register = max(register, buffer byte), PFMERGE semantics) and invalidates
+ * the cached cardinalities.  Both enqueue on `stream` (NULL = the context's) and return. */
+int rbx_hll_pack_registers(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n, void *d_buf, void *stream);
+int rbx_hll_unpack_max_registers(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n, const void *d_buf, void *stream);
+
 /* ---- multi-GPU (RCCL over xGMI) ------------------------------------------------------ */
 /* 128-byte ncclUniqueId, created on rank 0 and broadcast by the caller. */
 int rbx_rccl_unique_id(uint8_t out[128]);
 int rbx_rccl_init(rbx_ctx *ctx, const uint8_t id[128], int nranks, int rank);
-/* In-place uint8 MAX all-reduce of the registers of hlls[0..n) across ranks
- * (ncclAllReduce(ncclUint8, ncclMax)); every rank passes the same names in order. */
+/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank). */
+int rbx_rccl_info(rbx_ctx *ctx, int *nranks, int *rank);
+/* In-place uint8 MAX all-reduce of the registers of hlls[0..n) across ranks: pack (in the
+ * given order) -> ONE ncclAllReduce(ncclUint8, ncclMax) of n x 16384 bytes -> unpack_max, so
+ * every rank issues the same collective whatever its register pool layout.  Every rank passes
+ * the same names in the same order. */
 int rbx_hll_allreduce_max(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n);
 
 #ifdef __cplusplus

@@ -17,6 +17,13 @@ int rbx_bench_gather(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, ui
  * region_bytes-sized regions assigned round-robin by blockIdx % 8 (XCD affinity). */
 int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, uint64_t region_bytes,
                              uint64_t nlanes, unsigned grid, void *d_sink, void *stream);
+/* Stream-read roofline probe: reads `bytes` (16-byte aligned buffer) with 16-byte loads. */
+int rbx_bench_stream_read(rbx_ctx *ctx, const void *d_buf, uint64_t bytes, void *d_sink, void *stream);
+/* Segment-local gather probe (the locality of a multi-tenant batch): key i belongs to segment
+ * i / keys_per_segment, a consecutive segment_bytes slice of the table (wrapping), and does 4
+ * random 4-byte loads inside it. */
+int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, uint64_t segment_bytes,
+                              uint64_t keys_per_segment, uint64_t nkeys, void *d_sink, void *stream);
 /* Process-wide tuning knobs (results never change; A/B runs and tests only):
  *   "contains_stage1"       early-exit schedule of contains: 0 = all k gathers at once,
  *                           1..3 = that many bits first, 4 = doubling 1,2,4,... (default),

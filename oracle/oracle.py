@@ -58,6 +58,9 @@ def _load():
         "orc_hll_count": (C.c_uint64, [u8p]),
         "orc_hll_merge": (None, [u8p, u8p]),
         "orc_murmur_batch": (None, [u8p, u64p, C.c_uint64, u64p]),
+        "orc_bloom_contains_mt": (C.c_int64, [u8p, C.c_uint64, u8p, u64p, C.c_uint64, C.c_int, C.c_int64, u8p,
+                                              C.c_int]),
+        "orc_bloom_add_mt": (C.c_int64, [u8p, u64p, u8p, u64p, C.c_uint64, C.c_int, C.c_int64, u8p, C.c_int]),
         "orc_hash128_batch": (None, [u8p, u64p, C.c_uint64, u64p]),
     }
     for name, (res, args) in sig.items():
@@ -162,8 +165,8 @@ class OracleBloom:
     """A Redis bitmap string + Redisson's add/contains/count semantics."""
 
     def __init__(self, size: int, k: int):
-        self.size, self.k = int(size), int(k)
-        self.bitmap = np.zeros((self.size + 7) // 8 + 1, dtype=np.uint8)
+        self.size, self.k = int(size), int(k)  # size: the Java long (negative sizes index [0, |size|))
+        self.bitmap = np.zeros((abs(self.size) + 7) // 8 + 1, dtype=np.uint8)
         self.redis_len = 0
 
     def add(self, buf, offs, per_key: bool = False):
@@ -180,6 +183,23 @@ class OracleBloom:
         out = np.zeros(max(n, 1), np.uint8)
         c = lib().orc_bloom_contains(_p(self.bitmap), self.redis_len, _p(buf), _p(offs, u64p), n,
                                      self.k, self.size, _p(out))
+        return (c, out[:n]) if per_key else c
+
+    def add_mt(self, buf, offs, nthreads: int, per_key: bool = False):
+        """add() on nthreads threads (rbx_oracle_mt.c): the same flags, count and bitmap."""
+        n = offs.size - 1
+        out = np.zeros(max(n, 1), np.uint8)
+        rl = C.c_uint64(self.redis_len)
+        c = lib().orc_bloom_add_mt(_p(self.bitmap), C.byref(rl), _p(buf), _p(offs, u64p), n, self.k, self.size,
+                                   _p(out), int(nthreads))
+        self.redis_len = rl.value
+        return (c, out[:n]) if per_key else c
+
+    def contains_mt(self, buf, offs, nthreads: int, per_key: bool = False):
+        n = offs.size - 1
+        out = np.zeros(max(n, 1), np.uint8)
+        c = lib().orc_bloom_contains_mt(_p(self.bitmap), self.redis_len, _p(buf), _p(offs, u64p), n, self.k,
+                                        self.size, _p(out) if per_key else None, int(nthreads))
         return (c, out[:n]) if per_key else c
 
     def bitcount(self) -> int:

@@ -218,7 +218,8 @@ int orc_bloom_optimal(int64_t n, double p, int64_t max_size, int64_t *size_out, 
     if (p < 0) return ORC_E_ILLEGAL_ARGUMENT;
     double pp = p;
     if (pp == 0) pp = 4.9e-324; /* Double.MIN_VALUE */
-    int64_t size = java_d2l((double)(-n) * log(pp) / (log(2.0) * log(2.0)));
+    /* (double)(-n): Java's wrapping negation of a long */
+    int64_t size = java_d2l((double)(int64_t)(0 - (uint64_t)n) * log(pp) / (log(2.0) * log(2.0)));
     if (size == 0) return ORC_E_ILLEGAL_ARGUMENT;
     if (size > max_size) return ORC_E_ILLEGAL_ARGUMENT;
     /* optimalNumOfHashFunctions: Math.max(1, (int) Math.round((double) m / n * Math.log(2))) */
@@ -230,11 +231,13 @@ int orc_bloom_optimal(int64_t n, double p, int64_t max_size, int64_t *size_out, 
     return ORC_OK;
 }
 
-/* RedissonBloomFilter.java:139-151 */
+/* RedissonBloomFilter.java:139-151.  Java's `x % size` for x >= 0 takes the divisor's magnitude:
+ * a negative size (tryInit with a negative expectedInsertions) indexes [0, |size|). */
 void orc_bloom_indexes(uint64_t hash1, uint64_t hash2, int iterations, int64_t size, int64_t *out) {
     uint64_t hash = hash1;
+    const uint64_t m = size < 0 ? 0 - (uint64_t)size : (uint64_t)size;
     for (int i = 0; i < iterations; i++) {
-        out[i] = (int64_t)((hash & 0x7fffffffffffffffULL) % (uint64_t)size);
+        out[i] = (int64_t)((hash & 0x7fffffffffffffffULL) % m);
         if (i % 2 == 0) hash += hash2;
         else hash += hash1;
     }

@@ -24,9 +24,33 @@ class RbxKeys(C.Structure):
     _fields_ = [("bytes", vp), ("offsets", vp), ("stride", C.c_uint64), ("n", C.c_uint64)]
 
 
+class RbxName(C.Structure):
+    """struct rbx_name {bytes, len}: a binary-safe key name"""
+
+    _fields_ = [("bytes", vp), ("len", C.c_uint64)]
+
+
+def names_array(names):
+    """(rbx_name[], keep-alive buffers) for a list of bytes/str names."""
+    bufs = [n.encode("utf-8") if isinstance(n, str) else bytes(n) for n in names]
+    arr = (RbxName * max(len(bufs), 1))()
+    keep = []
+    for i, b in enumerate(bufs):
+        cb = C.create_string_buffer(b, len(b) or 1)
+        keep.append(cb)
+        arr[i].bytes = C.cast(cb, vp)
+        arr[i].len = len(b)
+    return arr, keep
+
+
+def name_struct(name):
+    arr, keep = names_array([name])
+    return arr[0], keep
+
+
 class RbxBloomConfig(C.Structure):
     _fields_ = [
-        ("size", C.c_uint64),
+        ("size", C.c_int64),
         ("hash_iterations", C.c_uint32),
         ("expected_insertions", C.c_int64),
         ("false_probability", C.c_double),
@@ -43,6 +67,7 @@ RBX_E_WRONGTYPE = -5
 RBX_E_DEVICE = -6
 RBX_E_OOM = -7
 RBX_E_NO_SUCH_KEY = -8
+RBX_E_REDIS = -9
 
 # name -> (restype, argtypes); every function declared in include/rbx.h
 SIGNATURES = {
@@ -59,7 +84,7 @@ SIGNATURES = {
     "rbx_crc16": (C.c_uint16, [u8p, C.c_size_t]),
     "rbx_calc_slot": (C.c_int, [u8p, C.c_size_t]),
     "rbx_slot_to_gpu": (C.c_int, [C.c_int, C.c_int]),
-    "rbx_bloom_optimal_config": (C.c_int, [C.c_int64, C.c_double, u64p, u32p]),
+    "rbx_bloom_optimal_config": (C.c_int, [C.c_int64, C.c_double, C.POINTER(C.c_int64), u32p]),
     "rbx_bloom_try_init": (C.c_int, [vp, C.c_char_p, C.c_int64, C.c_double, C.POINTER(C.c_int)]),
     "rbx_bloom_init_raw": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_int)]),
     "rbx_bloom_read_config": (C.c_int, [vp, C.c_char_p, C.POINTER(RbxBloomConfig)]),
@@ -107,6 +132,27 @@ SIGNATURES = {
     "rbx_rccl_unique_id": (C.c_int, [u8p]),
     "rbx_rccl_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
     "rbx_hll_allreduce_max": (C.c_int, [vp, C.POINTER(vp), C.c_uint32]),
+    "rbx_rccl_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
+    "rbx_bench_gather_segments": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp]),
+    # binary names (rbx_name)
+    "rbx_bloom_try_init_n": (C.c_int, [vp, RbxName, C.c_int64, C.c_double, C.POINTER(C.c_int)]),
+    "rbx_bloom_read_config_n": (C.c_int, [vp, RbxName, C.POINTER(RbxBloomConfig)]),
+    "rbx_bloom_add_n": (C.c_int, [vp, RbxName, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_contains_n": (C.c_int, [vp, RbxName, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_bloom_count_n": (C.c_int, [vp, RbxName, C.POINTER(C.c_int64)]),
+    "rbx_bloom_open_n": (C.c_int, [vp, RbxName, C.POINTER(vp)]),
+    "rbx_del_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_exists_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_pexpire_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+    "rbx_hll_add_multi_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
+    "rbx_hll_count_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p]),
+    "rbx_hll_merge_n": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
+    "rbx_hll_export_enc_n": (C.c_int, [vp, RbxName, C.c_int, u8p, C.c_uint64, u64p]),
+    "rbx_hll_import_n": (C.c_int, [vp, RbxName, u8p, C.c_uint64]),
+    "rbx_hll_open_n": (C.c_int, [vp, RbxName, C.c_int, C.POINTER(vp)]),
+    "rbx_hll_pack_registers": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, vp]),
+    "rbx_hll_unpack_max_registers": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, vp]),
     "rbx_bench_gather": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, vp]),
     "rbx_tune": (C.c_int, [C.c_char_p, C.c_int]),
     "rbx_bench_gather_regions": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint, vp, vp]),

@@ -1373,6 +1373,65 @@ __global__ __launch_bounds__(256) void k_gather_regions(const uint32_t *__restri
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Segment-local gather probe (the locality of a multi-tenant batch, BASELINE C3): key i belongs
+// to segment i / keys_per_seg, segments are consecutive slices of seg_words words (wrapping over
+// the table), and every key does K random 4-byte loads inside its own segment.
+template <int K>
+__global__ __launch_bounds__(256) void k_gather_segments(const uint32_t *__restrict__ tbl, uint64_t nwords,
+                                                         uint64_t seg_words, uint64_t keys_per_seg, uint64_t nkeys,
+                                                         uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    const uint64_t nseg_tbl = nwords / seg_words;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += stride) {
+        const uint32_t *base = tbl + ((i / keys_per_seg) % nseg_tbl) * seg_words;
+        uint64_t z = (i + 0x5EEDull) * 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z ^= z >> 27;
+        uint32_t w[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t r = (uint32_t)(z >> (j & 1 ? 32 : 0)) ^ (uint32_t)(j * 0x9E3779B9u);
+            z += 0x632BE59BD9B4E019ULL;
+            w[j] = base[(uint64_t)r * seg_words >> 32];
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc ^= w[j];
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+void launch_gather_segments(const uint32_t *tbl, uint64_t nwords, uint64_t seg_words, uint64_t keys_per_seg,
+                            uint64_t nkeys, uint32_t *sink, hipStream_t st) {
+    const unsigned grid = grid_for(nkeys, kMaxGrid);
+    hipLaunchKernelGGL(k_gather_segments<4>, dim3(grid), dim3(256), 0, st, tbl, nwords, seg_words, keys_per_seg,
+                       nkeys, sink);
+}
+
+// Streaming-read roofline probe: 16-byte loads of a whole buffer, 4 in flight per lane.
+__global__ __launch_bounds__(256) void k_stream_read(const u32x4 *__restrict__ src, uint64_t n16,
+                                                     uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) {
+        const u32x4 v = src[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_read, dim3(4096), dim3(256), 0, st, (const u32x4 *)buf, bytes / 16, sink);
+}
+
 void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
                            uint32_t *sink, hipStream_t st, unsigned grid) {
     const uint64_t nregions = nwords / region_words;

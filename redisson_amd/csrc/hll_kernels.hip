@@ -193,4 +193,23 @@ void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipSt
     hipLaunchKernelGGL(k_hll_merge, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, out, d_srcs, nsrc, 1);
 }
 
+// ---------------------------------------------------------------------------------
+// register exchange: HLL i <-> buf[i * 16384 ..], one block per HLL, 16 B per lane
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hll_pack(uint8_t *const *__restrict__ regs, uint8_t *__restrict__ buf,
+                                                  int unpack_max) {
+    u8x16 *r = (u8x16 *)regs[blockIdx.x];
+    u8x16 *b = (u8x16 *)(buf + (size_t)blockIdx.x * kHllRegs);
+#pragma unroll
+    for (int i = threadIdx.x; i < kHllRegs / 16; i += 256) {
+        if (unpack_max) r[i] = __builtin_elementwise_max(r[i], b[i]);
+        else b[i] = r[i];
+    }
+}
+
+void launch_hll_pack(uint8_t *const *d_regs, uint32_t n, uint8_t *buf, bool unpack_max, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_hll_pack, dim3(n), dim3(256), 0, st, d_regs, buf, unpack_max ? 1 : 0);
+}
+
 }  // namespace rbx

@@ -145,6 +145,12 @@ void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *
 // region-local gathers: 6 loads per lane inside XCD-assigned regions (partitioned-probe roofline)
 void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
                            uint32_t *sink, hipStream_t st, unsigned grid);
+// 4 random 4-byte gathers per key inside the key's segment (keys_per_seg consecutive keys share
+// one seg_words slice): the request roofline of multi-tenant batches at their locality
+void launch_gather_segments(const uint32_t *tbl, uint64_t nwords, uint64_t seg_words, uint64_t keys_per_seg,
+                            uint64_t nkeys, uint32_t *sink, hipStream_t st);
+// streaming 16-byte reads of a whole buffer: the HBM stream-read roofline probe
+void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStream_t st);
 // random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe
 void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
                          hipStream_t st);
@@ -173,5 +179,7 @@ void launch_hll_count(uint8_t *const *d_regs, uint32_t n, int *d_histo, unsigned
 void launch_hll_merge(uint8_t *dst, uint8_t *const *d_srcs, uint32_t nsrc, hipStream_t st);
 // raw registers -> scratch union: out = max over a set of HLLs (multi-key PFCOUNT)
 void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipStream_t st);
+// buf[i*16384..] = regs[i] (pack) or regs[i] = max(regs[i], buf[i*16384..]) (unpack_max)
+void launch_hll_pack(uint8_t *const *d_regs, uint32_t n, uint8_t *buf, bool unpack_max, hipStream_t st);
 
 }  // namespace rbx

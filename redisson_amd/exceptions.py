@@ -37,6 +37,7 @@ def raise_for(code: int, msg: str) -> None:
         L.RBX_E_ARITHMETIC: ArithmeticException,
         L.RBX_E_WRONGTYPE: RedisException,
         L.RBX_E_NO_SUCH_KEY: RedisException,
+        L.RBX_E_REDIS: RedisException,
         L.RBX_E_OOM: DeviceError,
         L.RBX_E_DEVICE: DeviceError,
     }.get(code, RedissonAmdError)

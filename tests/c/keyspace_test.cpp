@@ -1,0 +1,246 @@
+// keyspace_test.cpp -- host-only test of redisson_amd/csrc/keyspace.cpp (the part of librbx.so
+// that never touches a device), built with g++ under -fsanitize=address,undefined and, as a
+// second binary, -fsanitize=thread (tests/test_sanitizers.py).
+//
+// Device objects are stand-ins here: keyspace.h only holds them through shared_ptr, so this
+// file defines rbx::Bitmap / rbx::HllState as plain host structs that count their lifetimes.
+//
+//   1. Redisson Bloom config rules: the T/RedissonBloomFilterTest.java testConfig KAT
+//      (tryInit(100, 0.03) -> 729 bits, 5 hashes, "0.03"), a second tryInit returning false,
+//      IllegalArgumentException cases, and negative expectedInsertions (accepted, negative size).
+//   2. DEL / EXISTS / RENAME / RENAMENX key semantics on {name} + {name}:config.
+//   3. RExpirable timeouts against a fake clock: NX/XX/GT/LT, lazy expiry, sweep, PTTL/PEXPIRETIME.
+//   4. Concurrency: 8 threads issue random tryInit / addConfigCheck / rename / renamenx / delete /
+//      pexpire / persist / pttl / exists mixes on 24 shared names plus object creation and
+//      handle-style re-resolution -- include/rbx.h promises "calls from several threads are safe".
+// Exit code 0 and "ok" on stdout = every check passed.
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "../../include/rbx.h"
+#include "../../redisson_amd/csrc/keyspace.h"
+
+static std::atomic<long> g_live_bitmaps{0}, g_live_hlls{0};
+
+namespace rbx {
+struct Bitmap {
+    std::vector<uint8_t> bytes;
+    Bitmap() { g_live_bitmaps++; }
+    ~Bitmap() { g_live_bitmaps--; }
+};
+struct HllState {
+    uint8_t regs[64] = {0};
+    HllState() { g_live_hlls++; }
+    ~HllState() { g_live_hlls--; }
+};
+}  // namespace rbx
+
+using namespace rbx;
+
+static int g_fails = 0;
+#define CHECK(c)                                                                                  \
+    do {                                                                                          \
+        if (!(c)) {                                                                               \
+            fprintf(stderr, "FAIL %s:%d %s (%s)\n", __FILE__, __LINE__, #c, last_error_message()); \
+            g_fails++;                                                                            \
+        }                                                                                         \
+    } while (0)
+
+static void test_config() {
+    Keyspace ks;
+    int created = -1;
+    CHECK(ks_bloom_try_init(ks, "filter", 100, 0.03, &created) == RBX_OK && created == 1);
+    BloomConfig cfg;
+    CHECK(ks_get_config(ks, "filter", &cfg) == RBX_OK);
+    CHECK(cfg.size == 729 && cfg.k == 5 && cfg.expected == 100 && cfg.fpp_str == "0.03");
+    CHECK(ks_bloom_try_init(ks, "filter", 101, 0.03, &created) == RBX_OK && created == 0);
+    CHECK(ks_config_check(ks, "filter", 729, 5) == RBX_OK);
+    CHECK(ks_config_check(ks, "filter", 730, 5) == RBX_E_CONFIG_CHANGED);
+    CHECK(ks_config_check(ks, "other", 729, 5) == RBX_E_CONFIG_CHANGED);
+    CHECK(ks_get_config(ks, "other", &cfg) == RBX_E_ILLEGAL_STATE);
+    CHECK(strcmp(last_error_message(), "Bloom filter is not initialized!") == 0);
+    CHECK(ks_bloom_try_init(ks, "bad", 1, 2.0, &created) == RBX_E_ILLEGAL_ARGUMENT);
+    CHECK(ks_bloom_try_init(ks, "bad", 1, -0.5, &created) == RBX_E_ILLEGAL_ARGUMENT);
+    CHECK(ks_bloom_try_init(ks, "bad", 0, 0.5, &created) == RBX_E_ILLEGAL_ARGUMENT);            // size 0
+    CHECK(ks_bloom_try_init(ks, "bad", 1LL << 40, 0.001, &created) == RBX_E_ILLEGAL_ARGUMENT);  // > max
+    // negative expectedInsertions: size < 0 passes `size > getMaxSize()` (:270-276)
+    CHECK(ks_bloom_try_init(ks, "neg", -100, 0.03, &created) == RBX_OK && created == 1);
+    CHECK(ks_get_config(ks, "neg", &cfg) == RBX_OK && cfg.size == -729 && cfg.k == 5);
+    CHECK(size_bits(cfg.size) == 729);
+    CHECK(ks_bloom_init_raw(ks, "raw", 1ULL << 32, 7, &created) == RBX_OK && created == 1);
+    CHECK(ks_bloom_init_raw(ks, "raw2", (1ULL << 32) + 1, 7, &created) == RBX_E_ILLEGAL_ARGUMENT);
+    // a config name with a hashtag keeps it: suffixName
+    CHECK(config_name("a{b}c") == "a{b}c:config" && config_name("abc") == "{abc}:config");
+    // Java formatting helpers
+    CHECK(java_plain_string(1e-4) == "0.00010" && java_plain_string(0.5) == "0.5");
+    CHECK(java_math_round(2.5) == 3 && java_math_round(-2.5) == -2);
+    CHECK(calc_slot((const uint8_t *)"{user1000}.following", 20) == calc_slot((const uint8_t *)"user1000", 8));
+    CHECK(crc16((const uint8_t *)"123456789", 9) == 0x31C3);
+}
+
+static void put_bitmap(Keyspace &ks, const std::string &name) {
+    ks.put(name, Entry{KType::Bitmap, nullptr, std::make_shared<Bitmap>(), nullptr});
+    ks.generation++;
+}
+
+static void test_keys() {
+    Keyspace ks;
+    int created, n, e;
+    CHECK(ks_bloom_try_init(ks, "f", 1000, 0.01, &created) == RBX_OK);
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        put_bitmap(ks, "f");
+    }
+    CHECK(ks_bloom_is_exists(ks, "f", &e) == RBX_OK && e == 1);
+    CHECK(ks_bloom_rename(ks, "f", "g") == RBX_OK);
+    CHECK(ks_bloom_is_exists(ks, "f", &e) == RBX_OK && e == 0);
+    BloomConfig cfg;
+    CHECK(ks_get_config(ks, "g", &cfg) == RBX_OK && cfg.size == 9585);
+    CHECK(ks_bloom_rename(ks, "missing", "x") == RBX_E_NO_SUCH_KEY);
+    CHECK(ks_bloom_try_init(ks, "h", 1000, 0.01, &created) == RBX_OK);
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        put_bitmap(ks, "h");
+    }
+    int renamed = -1;
+    CHECK(ks_bloom_renamenx(ks, "g", "h", &renamed) == RBX_OK && renamed == 0);
+    CHECK(ks_bloom_renamenx(ks, "g", "i", &renamed) == RBX_OK && renamed == 1);
+    CHECK(ks_exists(ks, {"i", "{i}:config", "i", "g"}, &n) == RBX_OK && n == 3);
+    CHECK(ks_bloom_delete(ks, "i", &n) == RBX_OK && n == 2);
+    CHECK(ks_bloom_delete(ks, "i", &n) == RBX_OK && n == 0);
+    CHECK(ks_del(ks, {"h", "{h}:config", "nope"}, &n) == RBX_OK && n == 2);
+    CHECK(ks.size() == 0);
+    CHECK(g_live_bitmaps.load() == 0);
+}
+
+static void test_expiry() {
+    Keyspace ks;
+    int64_t now = 1'000'000;
+    ks.clock = [&]() { return now; };
+    int created, r;
+    int64_t t;
+    CHECK(ks_bloom_try_init(ks, "f", 1000, 0.01, &created) == RBX_OK);
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        put_bitmap(ks, "f");
+    }
+    const std::vector<std::string> both = {"f", "{f}:config"};
+    CHECK(ks_pttl(ks, "f", &t) == RBX_OK && t == -1);
+    CHECK(ks_pexpire(ks, both, 500, 0, 2 /*XX*/, &r) == RBX_OK && r == 0);
+    CHECK(ks_pexpire(ks, both, 500, 0, 1 /*NX*/, &r) == RBX_OK && r == 1);
+    CHECK(ks_pexpire(ks, both, 400, 0, 3 /*GT*/, &r) == RBX_OK && r == 0);
+    CHECK(ks_pexpire(ks, both, 400, 0, 4 /*LT*/, &r) == RBX_OK && r == 1);
+    CHECK(ks_pttl(ks, "f", &t) == RBX_OK && t == 400);
+    CHECK(ks_pexpiretime(ks, "{f}:config", &t) == RBX_OK && t == now + 400);
+    CHECK(ks_persist(ks, {"f"}, &r) == RBX_OK && r == 1);
+    CHECK(ks_pttl(ks, "f", &t) == RBX_OK && t == -1);
+    now += 399;
+    CHECK(ks_config_check(ks, "f", 9585, 7) == RBX_OK);
+    now += 1;  // the config's timeout passes; the bitmap is persistent
+    CHECK(ks_config_check(ks, "f", 9585, 7) == RBX_E_CONFIG_CHANGED);
+    CHECK(ks_pttl(ks, "{f}:config", &t) == RBX_OK && t == -2);
+    int e;
+    CHECK(ks_bloom_is_exists(ks, "f", &e) == RBX_OK && e == 1);
+    // a time not in the future deletes the key
+    CHECK(ks_pexpire(ks, {"f"}, now, 1, 0, &r) == RBX_OK && r == 1);
+    CHECK(ks_bloom_is_exists(ks, "f", &e) == RBX_OK && e == 0);
+    // sweep removes expired keys that nobody looks up
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        for (int i = 0; i < 10; ++i) put_bitmap(ks, "s" + std::to_string(i));
+    }
+    std::vector<std::string> ss;
+    for (int i = 0; i < 10; ++i) ss.push_back("s" + std::to_string(i));
+    CHECK(ks_pexpire(ks, ss, 10, 0, 0, &r) == RBX_OK && r == 1);
+    now += 10;
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        const uint64_t gen = ks.generation;
+        ks.sweep();
+        CHECK(ks.size() == 0 && ks.generation == gen + 10 && ks.next_expiry == INT64_MAX);
+    }
+    CHECK(g_live_bitmaps.load() == 0);
+}
+
+// A "handle": remembers the object it resolved and the generation it saw (rbx_api.cpp bloom_bind).
+struct FakeHandle {
+    std::string name;
+    std::shared_ptr<Bitmap> bm;
+    uint64_t gen = 0;
+};
+
+static void worker(Keyspace *ks, int tid, int iters, std::atomic<long> *ops) {
+    std::mt19937_64 rng(0x5EED + tid);
+    const int kNames = 24;
+    auto nm = [&](uint64_t x) { return "tenant:" + std::to_string(x % kNames); };
+    FakeHandle h{nm(tid), nullptr, 0};
+    for (int i = 0; i < iters; ++i) {
+        const uint64_t r = rng();
+        const std::string a = nm(r >> 8), b = nm(r >> 24);
+        int out = 0;
+        int64_t t = 0;
+        switch (r % 11) {
+        case 0: (void)ks_bloom_try_init(*ks, a, 1000 + (int64_t)(r % 3), 0.01, &out); break;
+        case 1: (void)ks_config_check(*ks, a, 9585, 7); break;
+        case 2: (void)ks_bloom_rename(*ks, a, b); break;
+        case 3: (void)ks_bloom_renamenx(*ks, a, b, &out); break;
+        case 4: (void)ks_bloom_delete(*ks, a, &out); break;
+        case 5: (void)ks_pexpire(*ks, {a, config_name(a)}, (int64_t)(r % 5), 0, (int)((r >> 40) % 5), &out); break;
+        case 6: (void)ks_persist(*ks, {a}, &out); break;
+        case 7: (void)ks_pttl(*ks, a, &t); break;
+        case 8: (void)ks_exists(*ks, {a, b}, &out); break;
+        case 9: {  // SETBIT's lazy creation of the bitmap key
+            std::lock_guard<std::recursive_mutex> g(ks->mu);
+            ks->sweep();
+            Entry *e = ks->find(a);
+            if (!e) put_bitmap(*ks, a);
+            break;
+        }
+        default: {  // handle re-resolution when the keyspace changed
+            std::lock_guard<std::recursive_mutex> g(ks->mu);
+            ks->sweep();
+            if (h.gen != ks->generation) {
+                Entry *e = ks->find(h.name);
+                h.bm = e && e->type == KType::Bitmap ? e->bm : nullptr;
+                h.gen = ks->generation;
+            }
+            if (h.bm) h.bm->bytes.push_back((uint8_t)r);  // the handle's object stays alive
+            if (h.bm && h.bm->bytes.size() > 64) h.bm->bytes.clear();
+            break;
+        }
+        }
+        ops->fetch_add(1, std::memory_order_relaxed);
+    }
+}
+
+static void test_concurrency() {
+    Keyspace ks;
+    std::atomic<long> ops{0};
+    std::vector<std::thread> th;
+    const int kThreads = 8, kIters = 20000;
+    for (int t = 0; t < kThreads; ++t) th.emplace_back(worker, &ks, t, kIters, &ops);
+    for (auto &x : th) x.join();
+    CHECK(ops.load() == (long)kThreads * kIters);
+    {
+        std::lock_guard<std::recursive_mutex> g(ks.mu);
+        ks.clear();
+    }
+    CHECK(g_live_bitmaps.load() == 0);
+}
+
+int main() {
+    test_config();
+    test_keys();
+    test_expiry();
+    test_concurrency();
+    if (g_fails) {
+        fprintf(stderr, "%d check(s) failed\n", g_fails);
+        return 1;
+    }
+    printf("keyspace_test: ok\n");
+    return 0;
+}

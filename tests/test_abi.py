@@ -72,7 +72,7 @@ def test_false_probability_plain_string():
 def test_error_mapping_without_gpu():
     from redisson_amd.exceptions import IllegalArgumentException, raise_for
 
-    s, k = C.c_uint64(), C.c_uint32()
+    s, k = C.c_int64(), C.c_uint32()
     rc = L.lib().rbx_bloom_optimal_config(1, 2.0, C.byref(s), C.byref(k))
     assert rc == L.RBX_E_ILLEGAL_ARGUMENT
     try:
@@ -90,3 +90,14 @@ def test_ttl_symbols_declared():
     hdr = open(os.path.join(ROOT, "include", "rbx.h")).read()
     for sym in ("rbx_pexpire", "rbx_persist", "rbx_pttl", "rbx_pexpiretime"):
         assert re.search(r"\b%s\(" % sym, hdr), sym
+
+
+def test_negative_expected_insertions_like_the_reference():
+    """tryInit(-n, p): optimalNumOfBits gives a negative size, which passes `size > getMaxSize()`
+    (M/RedissonBloomFilter.java:270-276) -- the config is created, as in the oracle."""
+    s, k = C.c_int64(), C.c_uint32()
+    for n, p in [(-100, 0.03), (-1, 0.5), (-10_000_000, 0.01)]:
+        assert L.lib().rbx_bloom_optimal_config(n, p, C.byref(s), C.byref(k)) == 0, (n, p)
+        want = O.bloom_optimal(n, p)
+        assert (s.value, k.value) == want, (n, p, s.value, k.value, want)
+        assert s.value < 0

@@ -128,3 +128,31 @@ def _bench_aggregation(rank, world):
 
 def test_bench_rank_aggregation_gloo():
     _run(_bench_aggregation)
+
+
+def test_bench_self_launches_n_ranks():
+    """`bench.py --gpus N` with no launcher starts N ranks itself (torch.distributed.run child),
+    each asserting WORLD_SIZE == N; --dry-run keeps it on the CPU (gloo)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 3 and d["ranks"] == 3 and len(set(d["pids"])) == 3
+
+
+def test_bench_refuses_world_mismatch():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])

@@ -173,3 +173,20 @@ def test_hll_sparse_pack_opcodes():
     for fill in (0.01, 0.2, 1.0):
         r = np.where(rng.random(16384) < fill, rng.integers(1, 33, 16384), 0).astype(np.uint8)
         assert np.array_equal(O.hll_sparse_unpack(O.hll_sparse_pack(r)), r)
+
+
+def test_multithreaded_restatement_matches_single_thread():
+    """rbx_oracle_mt.c (bench.py's all-core cpu_baseline) == rbx_oracle.c, per key and bitmap."""
+    rng = np.random.default_rng(31)
+    for size, k, n in [(9585, 7, 3000), (95_850_583, 7, 200_000), (-2000, 5, 1500), (64, 3, 500)]:
+        keys = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+        keys[n // 3: n // 3 + 50] = keys[:50]  # duplicates: only the first copy is new
+        a, b = O.OracleBloom(size, k), O.OracleBloom(size, k)
+        c1, f1 = a.add(*O.fixed_arena(keys), per_key=True)
+        c2, f2 = b.add_mt(*O.fixed_arena(keys), nthreads=7, per_key=True)
+        assert c1 == c2 and np.array_equal(f1, f2), (size, k)
+        assert a.redis_len == b.redis_len and a.redis_string() == b.redis_string()
+        probe = np.concatenate([keys[: n // 2], rng.integers(0, 256, size=(n, 16), dtype=np.uint8)])
+        r1 = a.contains(*O.fixed_arena(probe), per_key=True)
+        r2 = b.contains_mt(*O.fixed_arena(probe), nthreads=5, per_key=True)
+        assert r1[0] == r2[0] and np.array_equal(r1[1], r2[1])

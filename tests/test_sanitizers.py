@@ -1,8 +1,17 @@
-"""Host-only sanitizer run: the C oracle under ASan + UBSan.  CPU only."""
+"""Host-only sanitizer runs.  CPU only.
+
+- the C oracle under ASan + UBSan;
+- the HIP-free half of librbx.so (redisson_amd/csrc/keyspace.cpp: keyspace, Bloom config rules,
+  key timeouts, DEL/EXISTS/RENAME) under ASan + UBSan, and under TSan with 8 threads issuing
+  random tryInit / addConfigCheck / rename / renamenx / delete / pexpire / persist / pttl mixes
+  on shared names (include/rbx.h: "calls from several threads are safe")."""
 import os
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "redisson_amd", "csrc")
 
 
 def test_oracle_under_asan_ubsan():
@@ -11,3 +20,15 @@ def test_oracle_under_asan_ubsan():
                        timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+
+
+@pytest.mark.parametrize("flavor", ["asan", "tsan"])
+def test_keyspace_under_sanitizers(flavor):
+    target = f"../../tests/c/_build/keyspace_{flavor}"
+    subprocess.run(["make", "-s", "-C", CSRC, target], check=True)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1")
+    r = subprocess.run([os.path.join(ROOT, "tests", "c", "_build", f"keyspace_{flavor}")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "keyspace_test: ok" in r.stdout
+    assert "WARNING" not in r.stderr, r.stderr

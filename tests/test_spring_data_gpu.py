@@ -31,3 +31,27 @@ def test_pf_commands(client, fresh):
         conn.pfCount()
     with pytest.raises(IllegalArgumentException):
         conn.pfCount(k1, None)
+
+
+def test_pf_commands_binary_keys(client, fresh):
+    """byte[] keys may hold any byte (RedissonConnection.java:2203): keys that differ only after a
+    zero byte are distinct HLLs; the *_n entry points carry (bytes, length)."""
+    conn = RedissonConnection(client)
+    base = fresh.encode()
+    ka, kb = base + b"\x00a", base + b"\x00b"
+    rng = np.random.default_rng(2)
+    ea = [rng.bytes(16) for _ in range(500)]
+    eb = [rng.bytes(16) for _ in range(900)]
+    assert conn.pfAdd(ka, *ea) == 1
+    assert conn.pfAdd(kb, *eb) == 1
+    ra, rb = O.hll_new(), O.hll_new()
+    O.hll_pfadd(ra, *O.arena(ea))
+    O.hll_pfadd(rb, *O.arena(eb))
+    assert conn.pfCount(ka) == O.hll_count(ra)
+    assert conn.pfCount(kb) == O.hll_count(rb)
+    # the NUL-terminated form sees only the common prefix, which holds nothing
+    assert client.getHyperLogLog(fresh).count() == 0
+    conn.pfMerge(base + b"\x00\xff", ka, kb)
+    u = ra.copy()
+    O.hll_merge(u, rb)
+    assert conn.pfCount(base + b"\x00\xff") == O.hll_count(u)

@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic per launch from rocprofv3 --pmc CSVs -> profiles/traffic.json.
 
-Usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> [<hit_pass_dir>] -o profiles/traffic.json
+Usage: python tools/pmc_traffic.py <pass_dir>... -o profiles/traffic.json
+           [--calls pipeline=N ...] [--stream-bytes kernel=B ...]
 
-Follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB, collected in
-separate passes; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
-streaming read, so it is doubled ("x2 correction").  For these kernels most fetches are
-random 4-byte gathers (one 64-byte request each, uncalibrated width) -- the uncorrected
-figure is kept beside the corrected one and both are per launch, averaged over launches.
+Follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB, collected in separate
+passes; FETCH_SIZE = TCC_EA0_RDREQ x 64 B, and on gfx950 it reports exactly half the bytes of a
+wide coalesced streaming read (128-B requests tallied at 64 B).  The x2 correction therefore
+applies ONLY to streaming reads.  `hbm_bytes_by_class` prices each access class separately:
+  stream  kernels (every read a wide streaming read):  RDREQ x 128 B
+  gather  kernels (random 4-byte loads):               RDREQ x 64 B -- one 64-B request each
+  mixed   kernels (a key stream + random gathers):     S x 128 B + (RDREQ - S) x 64 B, with
+          S = the kernel's streamed bytes per launch / 128 (--stream-bytes, from the workload)
+plus WRITE_SIZE (exact for 16-B streaming stores).  Infinity-Cache hits are counted by these
+TCC counters, not excluded (the guide's note): for gather kernels over tables below 256 MiB
+the figure is an upper bound on DRAM bytes.  The old uniform "x2" figure stays beside it as
+`hbm_bytes_per_launch` (an over-count for gather kernels).
 """
 from __future__ import annotations
 
@@ -30,6 +38,12 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
          ("k_bloom_add_probe", r"k_bloom_add_probe"), ("k_bloom_add_commit", r"k_bloom_add_commit"),
          ("k_gather_probe", r"k_gather_probe"), ("k_hll_pfadd", r"k_hll_pfadd"), ("k_hll_count", r"k_hll_count"),
          ("k_bitcount", r"k_bitcount")]
+
+
+CLASS = {"k_bk_stage1": "mixed", "k_bloom_contains": "mixed", "k_bloom_contains_multi": "mixed",
+         "k_bloom_contains_q": "mixed", "k_stream_probe": "mixed", "k_stream_contains": "mixed",
+         "k_stream_commit": "mixed", "k_gather_probe": "gather", "k_bloom_add_probe": "gather",
+         "k_bloom_add_commit": "gather"}  # every other kernel: stream
 
 
 def short(name: str) -> str | None:
@@ -55,8 +69,11 @@ def main():
     ap.add_argument("-o", default="profiles/traffic.json")
     ap.add_argument("--calls", nargs="*", default=[],
                     help="pipeline=N: API calls of that pipeline in the profiled run (per-call totals)")
+    ap.add_argument("--stream-bytes", nargs="*", default=[],
+                    help="kernel=B: streamed (key) bytes per launch of a mixed-class kernel")
     a = ap.parse_args()
     calls = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.calls}
+    streamed = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in a.stream_bytes}
     merged = collections.defaultdict(dict)
     launches = {}
     for d in a.dirs:
@@ -83,6 +100,22 @@ def main():
         if "TCC_EA0_RDREQ_sum" in cs and "TCC_EA0_WRREQ_sum" in cs:
             # memory requests at the L2 -> EA interface (the binding rate for these kernels)
             e["requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"] + cs["TCC_EA0_WRREQ_sum"]
+        rd = cs.get("TCC_EA0_RDREQ_sum")
+        if rd is None and fetch is not None:
+            rd = fetch * 1024 / 64  # FETCH_SIZE = RDREQ x 64 B
+        if rd is not None and write is not None:
+            cls = CLASS.get(k, "stream")
+            if cls == "stream":
+                sb, gr = rd * 128, 0.0
+            elif cls == "gather":
+                sb, gr = 0.0, rd
+            else:
+                sb = streamed.get(k, 0.0)
+                gr = max(0.0, rd - sb / 128)
+            e["access_class"] = cls
+            e["read_bytes_stream"] = sb
+            e["read_requests_gather"] = gr
+            e["hbm_bytes_by_class"] = sb + 64 * gr + write * 1024
         out[k] = e
     for k in out:
         out[k]["launches_profiled"] = launches.get(k)
@@ -96,7 +129,8 @@ def main():
         agg = {"kernels": list(parts), "calls_profiled": calls[name],
                "note": "per API call: sum over the profiled launches / calls (the keys "
                        "written '_per_launch' here mean per call)"}
-        for f in ("hbm_bytes_per_launch", "requests_per_launch", "fetch_bytes_x2", "write_bytes"):
+        for f in ("hbm_bytes_per_launch", "hbm_bytes_by_class", "requests_per_launch", "fetch_bytes_x2",
+                  "write_bytes"):
             if all(f in out[k] for k in parts):
                 agg[f] = sum(out[k][f] * launches[k] for k in parts) / calls[name]
         out[name] = agg

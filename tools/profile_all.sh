@@ -1,13 +1,22 @@
 #!/bin/bash
-# Bench lines + rocprof kernel stats + PMC traffic for every workload -> gpurun_out/
+# rocprof kernel stats + PMC traffic for the C2 headline and the C3 / C4 legs -> gpurun_out/,
+# merged into gpurun_out/traffic_<tag>.json (copy to profiles/traffic.json to feed bench.py).
 # Run through gpurun:  bash tools/profile_all.sh <tag>
 set -u
-TAG=${1:-r01c}
+TAG=${1:-r02}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
-for w in c2 c3 c4 c5; do
-  timeout -k 10 400 python3 "$R/bench.py" --workload $w > "$R/gpurun_out/bench_${TAG}_$w.json" 2> "$R/gpurun_out/bench_${TAG}_$w.err" || exit 1
-  echo "bench $w ok"
-  timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_$w" --workload $w || exit 1
-done
+RBX_STREAM_BYTES="k_bk_stage1=3.2e9 k_bloom_contains=3.2e9" \
+  timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c2" --workload c2 || exit 1
+RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9" \
+  timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c3" --workload c3 || exit 1
+timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c4" --workload c4 || exit 1
+python3 - "$R/gpurun_out" "$TAG" <<'PY'
+import json, sys
+d, tag = sys.argv[1], sys.argv[2]
+out = {}
+for w in ("c2", "c3", "c4"):
+    out.update(json.load(open(f"{d}/profile_{tag}_{w}/traffic.json")))
+json.dump(out, open(f"{d}/traffic_{tag}.json", "w"), indent=1, sort_keys=True)
+PY
 echo "profile_all $TAG ok"
