@@ -45,13 +45,19 @@ enum {
     RBX_E_DEVICE = -6,           /* HIP / RCCL runtime failure                       */
     RBX_E_OOM = -7,              /* device or host allocation failure                */
     RBX_E_NO_SUCH_KEY = -8,      /* RedisException "ERR no such key" (RENAME)        */
-    RBX_E_REDIS = -9             /* other RedisException replies, e.g. "ERR bit offset is not an
+    RBX_E_REDIS = -9,            /* other RedisException replies, e.g. "ERR bit offset is not an
                                     integer or out of range" (a negative-size filter past 2^32 bits) */
+    RBX_E_TIMEOUT = -10          /* rbx_future_wait: the call has not completed in time        */
 };
 
 typedef struct rbx_ctx rbx_ctx;
 typedef struct rbx_bloom rbx_bloom;
 typedef struct rbx_hll rbx_hll;
+typedef struct rbx_future rbx_future;
+typedef struct rbx_node rbx_node;
+/* completion callback of an asynchronous call: rc = the call's return code (runs on the
+ * context's executor thread; a JVM binds it as an FFM upcall completing a CompletableFuture) */
+typedef void (*rbx_callback)(void *user, int rc);
 
 /* A batch of n encoded keys.  Key i is bytes[offsets[i] .. offsets[i+1]) when
  * offsets != NULL (n+1 entries), else bytes[i*stride .. (i+1)*stride). */
@@ -142,6 +148,11 @@ int rbx_bloom_count_n(rbx_ctx *ctx, rbx_name name, int64_t *out);
 /* DEL k1..kn (*deleted = keys removed) and EXISTS k1..kn (*count = existing keys, repeats
  * counted) over keys of any type -- RObject.delete / isExists for any name */
 int rbx_del_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, int *deleted);
+/* sizeInMemory (M/RedissonObject.java:124-130): bytes the engine holds for the existing keys --
+ * device allocation of a bitmap / HLL, config fields, key names (not Redis' allocator figures).
+ * The Bloom form sums the bitmap and {name}:config (M/RedissonBloomFilter.java:234-238). */
+int rbx_memory_usage_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, uint64_t *bytes);
+int rbx_bloom_size_in_memory(rbx_ctx *ctx, const char *name, uint64_t *bytes);
 int rbx_exists_n(rbx_ctx *ctx, const rbx_name *names, uint32_t n, int *count);
 /* BITCOUNT name */
 int rbx_bloom_bitcount(rbx_ctx *ctx, const char *name, uint64_t *out);
@@ -291,6 +302,69 @@ int rbx_rccl_info(rbx_ctx *ctx, int *nranks, int *rank);
  * every rank issues the same collective whatever its register pool layout.  Every rank passes
  * the same names in the same order. */
 int rbx_hll_allreduce_max(rbx_ctx *ctx, rbx_hll *const *hlls, uint32_t n);
+
+/* ---- asynchronous calls: the RFuture surface of RHyperLogLogAsync ---------------------------
+ * M/api/RHyperLogLogAsync.java:37-70 (addAsync, addAllAsync, countAsync, countWithAsync,
+ * mergeWithAsync; RBloomFilter has no async API in the reference -- the Bloom forms are an
+ * engine extension).  Each *_async call is queued on the context's serial executor and runs after
+ * every call queued before it on that context; it returns at once with a future.  Names, segment
+ * offsets and the rbx_keys descriptor are copied at submit time; key bytes and result buffers
+ * must stay valid until the future completes.  `cb` (nullable) runs when the call completes. */
+int rbx_future_wait(rbx_future *f, int64_t timeout_ms, int *call_rc); /* RBX_E_TIMEOUT if not done;
+                                                                         timeout_ms < 0 waits for ever */
+int rbx_future_done(rbx_future *f, int *done);
+int rbx_future_free(rbx_future *f);  /* may be called before completion (the result is dropped) */
+int rbx_bloom_add_async(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                        uint8_t *out_new, uint64_t *out_count, rbx_callback cb, void *user, rbx_future **out);
+int rbx_bloom_contains_async(rbx_ctx *ctx, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                             uint8_t *out_present, uint64_t *out_count, rbx_callback cb, void *user,
+                             rbx_future **out);
+int rbx_hll_add_async(rbx_ctx *ctx, const char *name, const rbx_keys *elements, int *changed, rbx_callback cb,
+                      void *user, rbx_future **out);
+int rbx_hll_add_multi_async(rbx_ctx *ctx, const char *const *names, uint32_t nseg, const uint64_t *seg_offsets,
+                            const rbx_keys *elements, uint8_t *out_changed, rbx_callback cb, void *user,
+                            rbx_future **out);
+int rbx_hll_count_async(rbx_ctx *ctx, const char *const *names, uint32_t n, uint64_t *result, rbx_callback cb,
+                        void *user, rbx_future **out);
+int rbx_hll_merge_async(rbx_ctx *ctx, const char *dest, const char *const *srcs, uint32_t nsrc, rbx_callback cb,
+                        void *user, rbx_future **out);
+
+/* ---- one process over the GPUs of a node -----------------------------------------------------
+ * A node holds one context per GPU and routes every name by Redis Cluster slot, the way the
+ * reference's client groups a batch per node (M/command/CommandBatchService.java:569-604,
+ * M/cluster/ClusterConnectionManager.java:777-830): GPU = calc_slot(name) * n_gpus / 16384, so a
+ * filter's bitmap `name` and its `{name}:config` live on one GPU.  devices: the HIP device of
+ * each of the n_gpus contexts (NULL = 0..n_gpus-1; a device may repeat, e.g. to rehearse a node
+ * on one GPU).  Multi-tenant batches are scattered by slot into per-GPU batches, run
+ * concurrently (one host thread per GPU, each GPU its own context and stream) and gathered back
+ * in segment order.  Calls on one node from several threads are safe. */
+int rbx_node_init(int n_gpus, const int *devices, rbx_node **out);
+int rbx_node_shutdown(rbx_node *node);
+int rbx_node_size(const rbx_node *node, int *n_gpus);
+int rbx_node_gpu_of(const rbx_node *node, rbx_name name, int *gpu);
+int rbx_node_ctx(rbx_node *node, int gpu, rbx_ctx **out); /* the GPU's context (device-path calls) */
+int rbx_node_bloom_try_init(rbx_node *node, rbx_name name, int64_t expected_insertions, double false_probability,
+                            int *created);
+int rbx_node_bloom_read_config(rbx_node *node, rbx_name name, rbx_bloom_config *out);
+int rbx_node_bloom_add(rbx_node *node, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                       uint8_t *out_new, uint64_t *out_count);
+int rbx_node_bloom_contains(rbx_node *node, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                            uint8_t *out_present, uint64_t *out_count);
+int rbx_node_bloom_count(rbx_node *node, rbx_name name, int64_t *out);
+int rbx_node_del(rbx_node *node, const rbx_name *names, uint32_t n, int *deleted);
+/* segment s = keys [seg_offsets[s], seg_offsets[s+1]) of names[s] (host buffers; a segment must
+ * be non-empty, as contains/add(Collection) of an empty collection throw); out_* nullable. */
+int rbx_node_bloom_contains_multi(rbx_node *node, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                                  const rbx_keys *keys, uint8_t *out_present, uint64_t *out_counts);
+int rbx_node_bloom_add_multi(rbx_node *node, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                             const rbx_keys *keys, uint8_t *out_new, uint64_t *out_counts);
+/* PFADD commands routed per name (commands on one name keep their order) */
+int rbx_node_hll_add_multi(rbx_node *node, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                           const rbx_keys *elements, uint8_t *out_changed);
+/* PFCOUNT / PFMERGE over names that may live on different GPUs: the registers of the other GPUs'
+ * HLLs are staged through the host (their Redis strings, encoding kept) */
+int rbx_node_hll_count(rbx_node *node, const rbx_name *names, uint32_t n, uint64_t *out);
+int rbx_node_hll_merge(rbx_node *node, rbx_name dest, const rbx_name *srcs, uint32_t nsrc);
 
 #ifdef __cplusplus
 }

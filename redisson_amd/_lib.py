@@ -68,6 +68,7 @@ RBX_E_DEVICE = -6
 RBX_E_OOM = -7
 RBX_E_NO_SUCH_KEY = -8
 RBX_E_REDIS = -9
+RBX_E_TIMEOUT = -10
 
 # name -> (restype, argtypes); every function declared in include/rbx.h
 SIGNATURES = {
@@ -133,6 +134,37 @@ SIGNATURES = {
     "rbx_rccl_init": (C.c_int, [vp, u8p, C.c_int, C.c_int]),
     "rbx_hll_allreduce_max": (C.c_int, [vp, C.POINTER(vp), C.c_uint32]),
     "rbx_rccl_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    # asynchronous calls (rbx_future)
+    "rbx_future_wait": (C.c_int, [vp, C.c_int64, C.POINTER(C.c_int)]),
+    "rbx_future_done": (C.c_int, [vp, C.POINTER(C.c_int)]),
+    "rbx_future_free": (C.c_int, [vp]),
+    "rbx_bloom_add_async": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), vp, vp, vp, vp,
+                                      C.POINTER(vp)]),
+    "rbx_bloom_contains_async": (C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), vp, vp, vp,
+                                           vp, C.POINTER(vp)]),
+    "rbx_hll_add_async": (C.c_int, [vp, C.c_char_p, C.POINTER(RbxKeys), vp, vp, vp, C.POINTER(vp)]),
+    "rbx_hll_add_multi_async": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, u64p, C.POINTER(RbxKeys), vp, vp,
+                                          vp, C.POINTER(vp)]),
+    "rbx_hll_count_async": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, vp, vp, vp, C.POINTER(vp)]),
+    "rbx_hll_merge_async": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32, vp, vp, C.POINTER(vp)]),
+    # one process over the GPUs of a node (rbx_node)
+    "rbx_node_init": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
+    "rbx_node_shutdown": (C.c_int, [vp]),
+    "rbx_node_size": (C.c_int, [vp, C.POINTER(C.c_int)]),
+    "rbx_node_gpu_of": (C.c_int, [vp, RbxName, C.POINTER(C.c_int)]),
+    "rbx_node_ctx": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
+    "rbx_node_bloom_try_init": (C.c_int, [vp, RbxName, C.c_int64, C.c_double, C.POINTER(C.c_int)]),
+    "rbx_node_bloom_read_config": (C.c_int, [vp, RbxName, C.POINTER(RbxBloomConfig)]),
+    "rbx_node_bloom_add": (C.c_int, [vp, RbxName, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_node_bloom_contains": (C.c_int, [vp, RbxName, C.c_uint64, C.c_uint32, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_node_bloom_count": (C.c_int, [vp, RbxName, C.POINTER(C.c_int64)]),
+    "rbx_node_del": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_node_bloom_contains_multi": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p,
+                                                u64p]),
+    "rbx_node_bloom_add_multi": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p, u64p]),
+    "rbx_node_hll_add_multi": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
+    "rbx_node_hll_count": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p]),
+    "rbx_node_hll_merge": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
     "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
     "rbx_bench_gather_segments": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp]),
     # binary names (rbx_name)
@@ -143,6 +175,8 @@ SIGNATURES = {
     "rbx_bloom_count_n": (C.c_int, [vp, RbxName, C.POINTER(C.c_int64)]),
     "rbx_bloom_open_n": (C.c_int, [vp, RbxName, C.POINTER(vp)]),
     "rbx_del_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.POINTER(C.c_int)]),
+    "rbx_memory_usage_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p]),
+    "rbx_bloom_size_in_memory": (C.c_int, [vp, C.c_char_p, u64p]),
     "rbx_exists_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.POINTER(C.c_int)]),
     "rbx_pexpire_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "rbx_hll_add_multi_n": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),

@@ -251,6 +251,12 @@ class RBloomFilter(_Expirable):
         _check(L.lib().rbx_bloom_is_exists(self._client.ctx, self._bname(), C.byref(e)))
         return bool(e.value)
 
+    def sizeInMemory(self) -> int:
+        """:234-238 -- the bitmap and the config hash (engine bytes)"""
+        out = C.c_uint64()
+        _check(L.lib().rbx_bloom_size_in_memory(self._client.ctx, self._bname(), C.byref(out)))
+        return int(out.value)
+
     def _expire_keys(self):
         # M/RedissonBloomFilter.java:303-314: the bitmap and its config hash
         return [self._name, _config_name(self._name)]
@@ -358,8 +364,46 @@ def bloom_stream(client: RedissonClient, handles: list[BloomHandle], key_filter,
     return out[: arena.n], counts
 
 
+class RFuture:
+    """org.redisson.api.RFuture over an rbx_future: the asynchronous call runs on the context's
+    serial executor; get() waits and returns the converted result (or raises the call's error)."""
+
+    def __init__(self, fut: C.c_void_p, convert, keep):
+        self._f = fut
+        self._convert = convert
+        self._keep = keep  # buffers the call reads / writes until it completes
+        self._done = False
+
+    def isDone(self) -> bool:
+        d = C.c_int()
+        _check(L.lib().rbx_future_done(self._f, C.byref(d)))
+        return bool(d.value)
+
+    def get(self, timeout_ms: int = -1):
+        """Result of the call; TimeoutError if it has not completed within timeout_ms."""
+        rc = C.c_int()
+        r = L.lib().rbx_future_wait(self._f, int(timeout_ms), C.byref(rc))
+        if r == L.RBX_E_TIMEOUT:
+            raise TimeoutError("the call has not completed")
+        _check(r)
+        _check(rc.value)
+        return self._convert()
+
+    def __del__(self):
+        f = getattr(self, "_f", None)
+        if f:
+            try:
+                L.lib().rbx_future_wait(f, -1, None)  # the buffers in _keep must outlive the call
+                L.lib().rbx_future_free(f)
+            except Exception:  # interpreter shutdown
+                pass
+
+    is_done = isDone
+
+
 class RHyperLogLog(_Expirable):
-    """M/RedissonHyperLogLog.java (PFADD / PFCOUNT / PFMERGE)."""
+    """M/RedissonHyperLogLog.java (PFADD / PFCOUNT / PFMERGE) and RHyperLogLogAsync
+    (M/api/RHyperLogLogAsync.java:37-70: the *Async methods return an RFuture)."""
 
     def __init__(self, client: RedissonClient, name: str, codec: Codec):
         self._client = client
@@ -396,6 +440,36 @@ class RHyperLogLog(_Expirable):
         """:97-102 PFMERGE name o1..on"""
         arr = (C.c_char_p * max(len(otherLogNames), 1))(*[n.encode() for n in otherLogNames])
         _check(L.lib().rbx_hll_merge(self._client.ctx, self._name.encode(), arr, len(otherLogNames)))
+
+    # ---- RHyperLogLogAsync ------------------------------------------------------------------
+    def addAsync(self, obj) -> RFuture:
+        return self.addAllAsync([obj])
+
+    def addAllAsync(self, objects) -> RFuture:
+        a = objects if isinstance(objects, Arena) else Arena([self._codec.encode(o) for o in objects])
+        ch = C.c_int()
+        f = C.c_void_p()
+        _check(L.lib().rbx_hll_add_async(self._client.ctx, self._name.encode(), a.ptr(), C.byref(ch), None, None,
+                                         C.byref(f)))
+        return RFuture(f, lambda: bool(ch.value), (a, ch))
+
+    def countAsync(self) -> RFuture:
+        return self.countWithAsync()
+
+    def countWithAsync(self, *otherLogNames: str) -> RFuture:
+        names = [self._name, *otherLogNames]
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        out = C.c_uint64()
+        f = C.c_void_p()
+        _check(L.lib().rbx_hll_count_async(self._client.ctx, arr, len(names), C.byref(out), None, None, C.byref(f)))
+        return RFuture(f, lambda: int(out.value), (arr, out))
+
+    def mergeWithAsync(self, *otherLogNames: str) -> RFuture:
+        arr = (C.c_char_p * max(len(otherLogNames), 1))(*[n.encode() for n in otherLogNames])
+        f = C.c_void_p()
+        _check(L.lib().rbx_hll_merge_async(self._client.ctx, self._name.encode(), arr, len(otherLogNames), None,
+                                           None, C.byref(f)))
+        return RFuture(f, lambda: None, (arr,))
 
     def delete(self) -> bool:
         n = C.c_int()
@@ -440,6 +514,9 @@ class RHyperLogLog(_Expirable):
     add_all = addAll
     count_with = countWith
     merge_with = mergeWith
+    add_all_async = addAllAsync
+    count_async = countAsync
+    merge_with_async = mergeWithAsync
 
 
 def hll_add_multi(client: RedissonClient, names: list[str], seg_offsets, arena: Arena) -> np.ndarray:

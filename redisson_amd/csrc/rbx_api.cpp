@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/rbx.h"
+#include "host_exec.h"
 #include "keyspace.h"
 #include "rbx_kernels.h"
 
@@ -207,6 +208,14 @@ struct rbx_ctx {
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
     hipEvent_t ev_scratch = nullptr;
     hipStream_t scratch_stream = nullptr;
+
+    // the asynchronous entry points' serial executor (host_exec.h): its thread starts with the
+    // first *_async call
+    std::unique_ptr<SerialExecutor> exec = std::make_unique<SerialExecutor>();
+};
+
+struct rbx_future {
+    std::shared_ptr<Future> f;
 };
 
 static void ctx_release(rbx_ctx *c) {
@@ -743,6 +752,8 @@ int rbx_init(int device, rbx_ctx **out) {
 // closed (closing a handle after shutdown is safe, every other call on it fails).
 int rbx_shutdown(rbx_ctx *c) {
     if (!c) return RBX_OK;
+    // queued asynchronous calls run to completion first (they take the context lock themselves)
+    if (c->exec) c->exec.reset();
     {
         std::lock_guard<std::recursive_mutex> g(c->ks.mu);
         if (c->shut) return fail(RBX_E_ILLEGAL_STATE, "the context has already been shut down");
@@ -2237,6 +2248,99 @@ int rbx_hll_allreduce_max(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n) {
     return hll_pack_locked(c, hlls, n, buf, true, c->stream);
 }
 
+// ---- asynchronous forms (RHyperLogLogAsync, M/api/RHyperLogLogAsync.java:37-70) ---------------
+// The call is queued on the context's serial executor (host_exec.h) and runs after every call
+// queued before it; names, segment offsets and the rbx_keys descriptor are copied at submit time,
+// key bytes and output buffers are read / written when the call runs (valid until completion).
+static int submit_async(rbx_ctx *c, std::function<int()> fn, rbx_callback cb, void *user, rbx_future **out) {
+    if (!c || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    {
+        std::lock_guard<std::recursive_mutex> g(c->ks.mu);
+        if (c->shut || !c->exec) return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
+    }
+    *out = new rbx_future{c->exec->submit(std::move(fn), cb, user)};
+    return RBX_OK;
+}
+
+int rbx_future_wait(rbx_future *f, int64_t timeout_ms, int *call_rc) {
+    if (!f) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL future");
+    if (!f->f->wait(timeout_ms)) return fail(RBX_E_TIMEOUT, "the call has not completed");
+    std::lock_guard<std::mutex> g(f->f->mu);
+    if (call_rc) *call_rc = f->f->rc;
+    if (f->f->rc) fail(f->f->rc, f->f->msg);  // rbx_last_error() on this thread = the call's message
+    return RBX_OK;
+}
+
+int rbx_future_done(rbx_future *f, int *done) {
+    if (!f || !done) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::mutex> g(f->f->mu);
+    *done = f->f->done;
+    return RBX_OK;
+}
+
+int rbx_future_free(rbx_future *f) {
+    delete f;  // the executor keeps its own reference until the call completes
+    return RBX_OK;
+}
+
+int rbx_bloom_add_async(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                        uint8_t *out_new, uint64_t *out_count, rbx_callback cb, void *user, rbx_future **out) {
+    if (!c || !name || !keys) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::string nm(name);
+    rbx_keys kc = *keys;
+    return submit_async(c, [=]() { return rbx_bloom_add(c, nm.c_str(), size, k, &kc, out_new, out_count); }, cb,
+                        user, out);
+}
+
+int rbx_bloom_contains_async(rbx_ctx *c, const char *name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                             uint8_t *out_present, uint64_t *out_count, rbx_callback cb, void *user,
+                             rbx_future **out) {
+    if (!c || !name || !keys) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::string nm(name);
+    rbx_keys kc = *keys;
+    return submit_async(c, [=]() { return rbx_bloom_contains(c, nm.c_str(), size, k, &kc, out_present, out_count); },
+                        cb, user, out);
+}
+
+// addAsync / addAllAsync (:71-81)
+int rbx_hll_add_async(rbx_ctx *c, const char *name, const rbx_keys *elements, int *changed, rbx_callback cb,
+                      void *user, rbx_future **out) {
+    if (!c || !name || !elements) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::string nm(name);
+    rbx_keys kc = *elements;
+    return submit_async(c, [=]() { return rbx_hll_add(c, nm.c_str(), &kc, changed); }, cb, user, out);
+}
+
+int rbx_hll_add_multi_async(rbx_ctx *c, const char *const *names, uint32_t nseg, const uint64_t *seg_offsets,
+                            const rbx_keys *elements, uint8_t *out_changed, rbx_callback cb, void *user,
+                            rbx_future **out) {
+    if (!c || !names || !seg_offsets || !elements) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::vector<std::string> v;
+    RBX_TRY(cstr_names(names, nseg, &v));
+    std::vector<uint64_t> seg(seg_offsets, seg_offsets + nseg + 1);
+    rbx_keys kc = *elements;
+    return submit_async(c, [=]() { return hll_add_multi(c, v, seg.data(), &kc, out_changed); }, cb, user, out);
+}
+
+// countAsync / countWithAsync (:84-94)
+int rbx_hll_count_async(rbx_ctx *c, const char *const *names, uint32_t n, uint64_t *result, rbx_callback cb,
+                        void *user, rbx_future **out) {
+    if (!c || !names || !result || n == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    std::vector<std::string> v;
+    RBX_TRY(cstr_names(names, n, &v));
+    return submit_async(c, [=]() { return hll_count(c, v, result); }, cb, user, out);
+}
+
+// mergeWithAsync (:97-102)
+int rbx_hll_merge_async(rbx_ctx *c, const char *dest, const char *const *srcs, uint32_t nsrc, rbx_callback cb,
+                        void *user, rbx_future **out) {
+    if (!c || !dest || (nsrc && !srcs)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::vector<std::string> v;
+    RBX_TRY(cstr_names(srcs, nsrc, &v));
+    std::string d(dest);
+    return submit_async(c, [=]() { return hll_merge(c, d, v); }, cb, user, out);
+}
+
 // ---- self test of the host-compiled device primitives (CPU tests call this) ------------
 // Returns the number of mismatches of mod63 against '%' over `n` pseudo-random pairs.
 uint64_t rbx_selftest_mod(uint64_t n, uint64_t seed) {
@@ -2349,6 +2453,37 @@ int rbx_set_staging(rbx_ctx *c, uint64_t bytes) {
     std::lock_guard<std::recursive_mutex> g(c->ks.mu);
     c->staging_bytes = bytes;
     return RBX_OK;
+}
+
+// ---- sizeInMemory (M/RedissonObject.java:124-130, Bloom: both keys, M/RedissonBloomFilter.java:234-238)
+// Bytes the engine holds for each existing key: a bitmap's device allocation (+ its 256-byte
+// length-word tail), an HLL's 16384 register bytes, a config hash's fields; plus the key name.
+// Redis' MEMORY USAGE reports its own allocator's figures, which no engine reproduces.
+static int memory_usage(rbx_ctx *c, const std::vector<std::string> &names, uint64_t *bytes) {
+    std::lock_guard<std::recursive_mutex> g(c->ks.mu);
+    uint64_t total = 0;
+    for (const auto &nm : names) {
+        Entry *e = c->ks.find(nm);
+        if (!e) continue;
+        total += nm.size();
+        if (e->type == KType::Bitmap) total += e->bm->cap_bytes + 256;
+        else if (e->type == KType::Hll) total += kHllBytes;
+        else total += sizeof(BloomConfig) + e->cfg->fpp_str.size();
+    }
+    *bytes = total;
+    return RBX_OK;
+}
+
+int rbx_memory_usage_n(rbx_ctx *c, const rbx_name *names, uint32_t n, uint64_t *bytes) {
+    if (!c || !bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::vector<std::string> v;
+    RBX_TRY(names_of(names, n, &v));
+    return memory_usage(c, v, bytes);
+}
+
+int rbx_bloom_size_in_memory(rbx_ctx *c, const char *name, uint64_t *bytes) {
+    if (!c || !name || !bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    return memory_usage(c, {std::string(name), config_name(name)}, bytes);
 }
 
 // ---- key timeouts (RedissonExpirable, M/RedissonExpirable.java:53-251; keyspace.cpp) ----------

@@ -1,0 +1,404 @@
+// rbx_node.cpp -- one process over the GPUs of a node (include/rbx.h, "one process over the GPUs
+// of a node").  A pure host-side router written against the public per-GPU C ABI: a node holds
+// one rbx_ctx per GPU and sends every name to GPU = calc_slot(name) * n_gpus / 16384, the slot
+// routing the reference's client applies per command
+// (M/cluster/ClusterConnectionManager.java:777-830) and per batch, where each node's commands
+// are grouped and sent together (M/command/CommandBatchService.java:569-604).
+//
+// Multi-tenant batches are scattered by slot into per-GPU host arenas, run concurrently (one host
+// thread per GPU with work; each GPU has its own context, stream and copy stream, so the PCIe
+// uploads and kernels of different GPUs overlap) and gathered back in segment order.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rbx.h"
+#include "keyspace.h"
+
+using namespace rbx;
+
+struct rbx_node {
+    std::vector<rbx_ctx *> ctx;
+    std::mutex mu;                                            // the handle cache
+    std::map<std::pair<int, std::string>, rbx_bloom *> blooms;  // open handles per (GPU, name)
+    std::vector<rbx_bloom *> retired;                         // replaced handles, closed at shutdown
+};
+
+static std::atomic<uint64_t> g_tmp_serial{1};
+
+static std::string str_of(const rbx_name &n) { return std::string((const char *)n.bytes, (size_t)n.len); }
+static rbx_name name_ref(const std::string &s) { return rbx_name{(const uint8_t *)s.data(), (uint64_t)s.size()}; }
+
+static int gpu_of(const rbx_node *nd, const std::string &name) {
+    return slot_to_gpu(calc_slot((const uint8_t *)name.data(), name.size()), (int)nd->ctx.size());
+}
+
+static int check_name(const rbx_name &n) {
+    if (!n.bytes && n.len) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key name");
+    return RBX_OK;
+}
+
+#define NODE_TRY(expr)                 \
+    do {                               \
+        const int r_ = (expr);         \
+        if (r_ != RBX_OK) return r_;   \
+    } while (0)
+
+// Runs fn(g) for every GPU g with work, concurrently when more than one; the first failure (in
+// GPU order) becomes this thread's error.
+template <class Fn>
+static int per_gpu(const std::vector<int> &gpus, Fn &&fn) {
+    struct Res {
+        int rc = RBX_OK;
+        std::string msg;
+    };
+    std::vector<Res> res(gpus.size());
+    auto run = [&](size_t i) {
+        res[i].rc = fn(gpus[i]);
+        if (res[i].rc != RBX_OK) res[i].msg = rbx_last_error();
+    };
+    if (gpus.size() == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < gpus.size(); ++i) th.emplace_back(run, i);
+        for (auto &t : th) t.join();
+    }
+    for (auto &r : res)
+        if (r.rc != RBX_OK) return fail(r.rc, r.msg);
+    return RBX_OK;
+}
+
+extern "C" {
+
+int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
+    if (!out || n_gpus < 1 || n_gpus > 16384) return fail(RBX_E_ILLEGAL_ARGUMENT, "n_gpus must be in [1, 16384]");
+    auto *nd = new rbx_node();
+    for (int i = 0; i < n_gpus; ++i) {
+        rbx_ctx *c = nullptr;
+        const int rc = rbx_init(devices ? devices[i] : i, &c);
+        if (rc != RBX_OK) {
+            const std::string msg = rbx_last_error();
+            for (rbx_ctx *p : nd->ctx) rbx_shutdown(p);
+            delete nd;
+            return fail(rc, msg);
+        }
+        nd->ctx.push_back(c);
+    }
+    *out = nd;
+    return RBX_OK;
+}
+
+int rbx_node_shutdown(rbx_node *nd) {
+    if (!nd) return RBX_OK;
+    for (auto &kv : nd->blooms) rbx_bloom_close(kv.second);
+    for (rbx_bloom *b : nd->retired) rbx_bloom_close(b);
+    int rc = RBX_OK;
+    for (rbx_ctx *c : nd->ctx) {
+        const int r = rbx_shutdown(c);
+        if (rc == RBX_OK) rc = r;
+    }
+    delete nd;
+    return rc;
+}
+
+int rbx_node_size(const rbx_node *nd, int *n) {
+    if (!nd || !n) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    *n = (int)nd->ctx.size();
+    return RBX_OK;
+}
+
+int rbx_node_gpu_of(const rbx_node *nd, rbx_name name, int *gpu) {
+    if (!nd || !gpu) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    NODE_TRY(check_name(name));
+    *gpu = gpu_of(nd, str_of(name));
+    return RBX_OK;
+}
+
+int rbx_node_ctx(rbx_node *nd, int gpu, rbx_ctx **out) {
+    if (!nd || !out || gpu < 0 || gpu >= (int)nd->ctx.size()) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    *out = nd->ctx[gpu];
+    return RBX_OK;
+}
+
+// ---- single objects: routed by slot -------------------------------------------------------------
+int rbx_node_bloom_try_init(rbx_node *nd, rbx_name name, int64_t n, double p, int *created) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    return rbx_bloom_try_init_n(nd->ctx[gpu_of(nd, str_of(name))], name, n, p, created);
+}
+
+int rbx_node_bloom_read_config(rbx_node *nd, rbx_name name, rbx_bloom_config *out) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    return rbx_bloom_read_config_n(nd->ctx[gpu_of(nd, str_of(name))], name, out);
+}
+
+int rbx_node_bloom_add(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                       uint8_t *out_new, uint64_t *out_count) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    return rbx_bloom_add_n(nd->ctx[gpu_of(nd, str_of(name))], name, size, k, keys, out_new, out_count);
+}
+
+int rbx_node_bloom_contains(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                            uint8_t *out_present, uint64_t *out_count) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    return rbx_bloom_contains_n(nd->ctx[gpu_of(nd, str_of(name))], name, size, k, keys, out_present, out_count);
+}
+
+int rbx_node_bloom_count(rbx_node *nd, rbx_name name, int64_t *out) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    return rbx_bloom_count_n(nd->ctx[gpu_of(nd, str_of(name))], name, out);
+}
+
+int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) {
+    if (!nd || (n && !names)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::vector<std::vector<rbx_name>> by(nd->ctx.size());
+    for (uint32_t i = 0; i < n; ++i) {
+        NODE_TRY(check_name(names[i]));
+        by[gpu_of(nd, str_of(names[i]))].push_back(names[i]);
+    }
+    int total = 0;
+    for (size_t g = 0; g < by.size(); ++g) {
+        if (by[g].empty()) continue;
+        int d = 0;
+        NODE_TRY(rbx_del_n(nd->ctx[g], by[g].data(), (uint32_t)by[g].size(), &d));
+        total += d;
+    }
+    if (deleted) *deleted = total;
+    return RBX_OK;
+}
+
+// ---- multi-tenant batches -------------------------------------------------------------------------
+// One GPU's share of a batch: its segments (in batch order) copied into a host arena.
+struct Part {
+    std::vector<uint32_t> segs;  // batch segment ids
+    std::vector<uint8_t> bytes;
+    std::vector<uint64_t> offs;  // variable-length arenas
+    std::vector<uint64_t> seg;   // local segment offsets
+    std::vector<uint8_t> out;
+    std::vector<uint64_t> cnt;
+    rbx_keys keys{};
+};
+
+static int validate_batch(const rbx_name *names, uint32_t nseg, const uint64_t *seg, const rbx_keys *keys) {
+    if (!names || !seg || !keys || nseg == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    if (keys->n && !keys->bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
+    if (seg[0] != 0 || seg[nseg] != keys->n) return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must span [0, n]");
+    for (uint32_t s = 0; s < nseg; ++s) {
+        if (seg[s + 1] < seg[s]) return fail(RBX_E_ILLEGAL_ARGUMENT, "segment offsets must be ascending");
+        NODE_TRY(check_name(names[s]));
+    }
+    return RBX_OK;
+}
+
+// scatter: every GPU's part of the batch, keys copied in segment order
+static void build_parts(const rbx_node *nd, const std::vector<std::string> &sn, const uint64_t *seg,
+                        const rbx_keys *keys, std::vector<Part> *parts) {
+    parts->assign(nd->ctx.size(), Part{});
+    for (uint32_t s = 0; s < sn.size(); ++s) (*parts)[gpu_of(nd, sn[s])].segs.push_back(s);
+    for (Part &p : *parts) {
+        if (p.segs.empty()) continue;
+        p.seg.push_back(0);
+        if (keys->offsets) p.offs.push_back(0);
+        for (uint32_t s : p.segs) {
+            const uint64_t i0 = seg[s], i1 = seg[s + 1];
+            if (keys->offsets) {
+                const uint64_t b0 = keys->offsets[i0], b1 = keys->offsets[i1];
+                const uint64_t base = p.bytes.size();
+                p.bytes.insert(p.bytes.end(), keys->bytes + b0, keys->bytes + b1);
+                for (uint64_t i = i0; i < i1; ++i) p.offs.push_back(base + keys->offsets[i + 1] - b0);
+            } else {
+                p.bytes.insert(p.bytes.end(), keys->bytes + i0 * keys->stride, keys->bytes + i1 * keys->stride);
+            }
+            p.seg.push_back(p.seg.back() + (i1 - i0));
+        }
+        if (p.bytes.empty()) p.bytes.push_back(0);
+        p.keys = rbx_keys{p.bytes.data(), keys->offsets ? p.offs.data() : nullptr, keys->stride, p.seg.back()};
+        p.out.resize(std::max<uint64_t>(p.seg.back(), 1));
+        p.cnt.resize(p.segs.size());
+    }
+}
+
+static std::vector<int> gpus_with_work(const std::vector<Part> &parts) {
+    std::vector<int> g;
+    for (size_t i = 0; i < parts.size(); ++i)
+        if (!parts[i].segs.empty()) g.push_back((int)i);
+    return g;
+}
+
+// the cached handle of (gpu, name); refresh = replace it with a freshly opened one (the config was
+// re-created with other parameters: a new RBloomFilter object would read the new config)
+static int bloom_handle(rbx_node *nd, int g, const std::string &name, bool refresh, rbx_bloom **out) {
+    std::lock_guard<std::mutex> lk(nd->mu);
+    auto key = std::make_pair(g, name);
+    auto it = nd->blooms.find(key);
+    if (it != nd->blooms.end() && !refresh) {
+        *out = it->second;
+        return RBX_OK;
+    }
+    rbx_bloom *b = nullptr;
+    NODE_TRY(rbx_bloom_open_n(nd->ctx[g], name_ref(name), &b));
+    if (it != nd->blooms.end()) {
+        nd->retired.push_back(it->second);  // another thread may still be using it
+        it->second = b;
+    } else {
+        nd->blooms[key] = b;
+    }
+    *out = b;
+    return RBX_OK;
+}
+
+static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const uint64_t *seg, const rbx_keys *keys,
+                       uint8_t *out, uint64_t *counts, bool is_add) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(validate_batch(names, nseg, seg, keys));
+    std::vector<std::string> sn(nseg);
+    for (uint32_t s = 0; s < nseg; ++s) sn[s] = str_of(names[s]);
+    std::vector<Part> parts;
+    build_parts(nd, sn, seg, keys, &parts);
+    const std::vector<int> gpus = gpus_with_work(parts);
+    const int rc = per_gpu(gpus, [&](int g) -> int {
+        Part &p = parts[g];
+        for (int attempt = 0;; ++attempt) {
+            std::vector<rbx_bloom *> hs(p.segs.size());
+            for (size_t j = 0; j < p.segs.size(); ++j) NODE_TRY(bloom_handle(nd, g, sn[p.segs[j]], attempt > 0, &hs[j]));
+            const auto fn = is_add ? rbx_bloom_add_multi : rbx_bloom_contains_multi;
+            const int r = fn(nd->ctx[g], hs.data(), (uint32_t)hs.size(), p.seg.data(), &p.keys,
+                             out ? p.out.data() : nullptr, p.cnt.data());
+            if (r != RBX_E_CONFIG_CHANGED || attempt > 0) return r;
+        }
+    });
+    if (rc != RBX_OK) return rc;
+    // gather in segment order
+    for (int g : gpus) {
+        const Part &p = parts[g];
+        for (size_t j = 0; j < p.segs.size(); ++j) {
+            const uint32_t s = p.segs[j];
+            if (counts) counts[s] = p.cnt[j];
+            if (out) memcpy(out + seg[s], p.out.data() + p.seg[j], seg[s + 1] - seg[s]);
+        }
+    }
+    return RBX_OK;
+}
+
+int rbx_node_bloom_contains_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                                  const rbx_keys *keys, uint8_t *out_present, uint64_t *out_counts) {
+    return bloom_multi(nd, names, nseg, seg_offsets, keys, out_present, out_counts, false);
+}
+
+int rbx_node_bloom_add_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                             const rbx_keys *keys, uint8_t *out_new, uint64_t *out_counts) {
+    return bloom_multi(nd, names, nseg, seg_offsets, keys, out_new, out_counts, true);
+}
+
+// ---- HyperLogLog ------------------------------------------------------------------------------
+int rbx_node_hll_add_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
+                           const rbx_keys *elements, uint8_t *out_changed) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(validate_batch(names, nseg, seg_offsets, elements));
+    std::vector<std::string> sn(nseg);
+    for (uint32_t s = 0; s < nseg; ++s) sn[s] = str_of(names[s]);
+    std::vector<Part> parts;
+    build_parts(nd, sn, seg_offsets, elements, &parts);
+    const std::vector<int> gpus = gpus_with_work(parts);
+    const int rc = per_gpu(gpus, [&](int g) -> int {
+        Part &p = parts[g];
+        std::vector<rbx_name> nm(p.segs.size());
+        for (size_t j = 0; j < p.segs.size(); ++j) nm[j] = name_ref(sn[p.segs[j]]);
+        return rbx_hll_add_multi_n(nd->ctx[g], nm.data(), (uint32_t)nm.size(), p.seg.data(), &p.keys, p.out.data());
+    });
+    if (rc != RBX_OK) return rc;
+    for (int g : gpus) {
+        const Part &p = parts[g];
+        for (size_t j = 0; j < p.segs.size(); ++j)
+            if (out_changed) out_changed[p.segs[j]] = p.out[j];
+    }
+    return RBX_OK;
+}
+
+// Names of other GPUs' HLLs as temporary keys on GPU `dst`: their Redis strings (encoding kept)
+// exported and imported there.  Missing keys are skipped (PFCOUNT / PFMERGE ignore them).
+static int stage_on(rbx_node *nd, int dst, const std::vector<std::string> &remote, std::vector<std::string> *tmps) {
+    std::vector<uint8_t> buf(16 + 12288);
+    for (const std::string &r : remote) {
+        uint64_t len = 0;
+        NODE_TRY(rbx_hll_export_enc_n(nd->ctx[gpu_of(nd, r)], name_ref(r), RBX_HLL_AS_STORED, buf.data(), buf.size(),
+                                      &len));
+        if (len == 0) continue;
+        // a binary name no client key is expected to take: NUL-prefixed, unique per call
+        std::string t = std::string("\0rbx-node-tmp:", 14) + std::to_string(g_tmp_serial++);
+        NODE_TRY(rbx_hll_import_n(nd->ctx[dst], name_ref(t), buf.data(), len));
+        tmps->push_back(t);
+    }
+    return RBX_OK;
+}
+
+static void drop(rbx_node *nd, int g, const std::vector<std::string> &tmps) {
+    if (tmps.empty()) return;
+    std::vector<rbx_name> v;
+    for (const auto &t : tmps) v.push_back(name_ref(t));
+    int d;
+    (void)rbx_del_n(nd->ctx[g], v.data(), (uint32_t)v.size(), &d);
+}
+
+int rbx_node_hll_count(rbx_node *nd, const rbx_name *names, uint32_t n, uint64_t *out) {
+    if (!nd || !names || !out || n == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL/empty argument");
+    std::vector<std::string> sn(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        NODE_TRY(check_name(names[i]));
+        sn[i] = str_of(names[i]);
+    }
+    const int g0 = gpu_of(nd, sn[0]);
+    std::vector<rbx_name> local;
+    std::vector<std::string> remote, tmps;
+    for (const auto &s : sn) {
+        if (gpu_of(nd, s) == g0) local.push_back(name_ref(s));
+        else remote.push_back(s);
+    }
+    if (remote.empty()) return rbx_hll_count_n(nd->ctx[g0], local.data(), (uint32_t)local.size(), out);
+    int rc = stage_on(nd, g0, remote, &tmps);
+    if (rc == RBX_OK) {
+        for (const auto &t : tmps) local.push_back(name_ref(t));
+        // >= 2 names: the union count, never a single key's cached cardinality
+        rc = rbx_hll_count_n(nd->ctx[g0], local.data(), (uint32_t)local.size(), out);
+    }
+    const std::string msg = rc ? rbx_last_error() : "";
+    drop(nd, g0, tmps);
+    return rc ? fail(rc, msg) : RBX_OK;
+}
+
+int rbx_node_hll_merge(rbx_node *nd, rbx_name dest, const rbx_name *srcs, uint32_t nsrc) {
+    if (!nd || (nsrc && !srcs)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    NODE_TRY(check_name(dest));
+    const std::string d = str_of(dest);
+    const int gd = gpu_of(nd, d);
+    std::vector<std::string> sn, remote, tmps;
+    for (uint32_t i = 0; i < nsrc; ++i) {
+        NODE_TRY(check_name(srcs[i]));
+        sn.push_back(str_of(srcs[i]));
+    }
+    std::vector<rbx_name> local;
+    for (const auto &s : sn) {
+        if (gpu_of(nd, s) == gd) local.push_back(name_ref(s));
+        else remote.push_back(s);
+    }
+    int rc = stage_on(nd, gd, remote, &tmps);
+    if (rc == RBX_OK) {
+        for (const auto &t : tmps) local.push_back(name_ref(t));
+        rc = rbx_hll_merge_n(nd->ctx[gd], dest, local.data(), (uint32_t)local.size());
+    }
+    const std::string msg = rc ? rbx_last_error() : "";
+    drop(nd, gd, tmps);
+    return rc ? fail(rc, msg) : RBX_OK;
+}
+
+}  // extern "C"

@@ -10,6 +10,9 @@
 //      IllegalArgumentException cases, and negative expectedInsertions (accepted, negative size).
 //   2. DEL / EXISTS / RENAME / RENAMENX key semantics on {name} + {name}:config.
 //   3. RExpirable timeouts against a fake clock: NX/XX/GT/LT, lazy expiry, sweep, PTTL/PEXPIRETIME.
+//   5. The asynchronous calls' serial executor (host_exec.cpp): 6 threads submit 2000 calls each to
+//      one executor; calls run one at a time in submission order per submitter, every future
+//      completes with its code and message, callbacks run, waits with timeouts behave.
 //   4. Concurrency: 8 threads issue random tryInit / addConfigCheck / rename / renamenx / delete /
 //      pexpire / persist / pttl / exists mixes on 24 shared names plus object creation and
 //      handle-style re-resolution -- include/rbx.h promises "calls from several threads are safe".
@@ -22,6 +25,7 @@
 #include <vector>
 
 #include "../../include/rbx.h"
+#include "../../redisson_amd/csrc/host_exec.h"
 #include "../../redisson_amd/csrc/keyspace.h"
 
 static std::atomic<long> g_live_bitmaps{0}, g_live_hlls{0};
@@ -232,7 +236,70 @@ static void test_concurrency() {
     CHECK(g_live_bitmaps.load() == 0);
 }
 
+static std::atomic<int> g_cb_calls{0};
+static void on_done(void *user, int rc) {
+    g_cb_calls++;
+    if (user) *(int *)user = rc;
+}
+
+static void test_executor() {
+    std::atomic<int> running{0}, overlap{0};
+    std::vector<long> last(6, -1);
+    std::atomic<long> order_errors{0};
+    {
+        SerialExecutor ex;
+        std::vector<std::thread> th;
+        std::vector<std::vector<std::shared_ptr<Future>>> futs(6);
+        for (int t = 0; t < 6; ++t) {
+            th.emplace_back([&, t]() {
+                for (long i = 0; i < 2000; ++i) {
+                    futs[t].push_back(ex.submit(
+                        [&, t, i]() -> int {
+                            if (running.fetch_add(1) != 0) overlap++;
+                            if (last[t] != i - 1) order_errors++;  // one submitter's calls stay in order
+                            last[t] = i;
+                            running.fetch_sub(1);
+                            if (i % 97 == 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "call " + std::to_string(i));
+                            return RBX_OK;
+                        },
+                        i % 5 == 0 ? on_done : nullptr, nullptr));
+                }
+            });
+        }
+        for (auto &x : th) x.join();
+        ex.drain();
+        for (int t = 0; t < 6; ++t) {
+            for (long i = 0; i < 2000; ++i) {
+                Future &f = *futs[t][i];
+                CHECK(f.wait(0));
+                const bool bad = i % 97 == 0;
+                CHECK(f.rc == (bad ? RBX_E_ILLEGAL_ARGUMENT : RBX_OK));
+                if (bad) CHECK(f.msg == "call " + std::to_string(i));
+            }
+        }
+        // a long call: a short wait times out, a full wait completes; the callback gets rc
+        int cb_rc = 12345;
+        std::atomic<bool> release{false};
+        auto slow = ex.submit(
+            [&]() -> int {
+                while (!release.load()) std::this_thread::yield();
+                return RBX_E_NO_SUCH_KEY;
+            },
+            on_done, &cb_rc);
+        CHECK(!slow->wait(5));
+        release = true;
+        CHECK(slow->wait(-1) && slow->rc == RBX_E_NO_SUCH_KEY);
+        ex.drain();
+        CHECK(cb_rc == RBX_E_NO_SUCH_KEY);
+        // queued work still runs when the executor is destroyed
+        for (int i = 0; i < 50; ++i) ex.submit([&]() -> int { return RBX_OK; }, on_done, nullptr);
+    }
+    CHECK(overlap.load() == 0 && order_errors.load() == 0);
+    CHECK(g_cb_calls.load() == 6 * 400 + 1 + 50);
+}
+
 int main() {
+    test_executor();
     test_config();
     test_keys();
     test_expiry();

@@ -50,3 +50,15 @@ def test_rccl_single_rank_max_allreduce(client, fresh):
         assert np.array_equal(O.hll_dense_unpack(d[16:]), r)
     for h in hs:
         L.lib().rbx_hll_close(h)
+
+
+def test_java_ffm_shim_replay():
+    """INTEGRATION.md's Java FFM shim, replayed from C: struct offsets of rbx_keys /
+    rbx_bloom_config / rbx_name as the Java StructLayouts declare them, and each shim method's
+    downcall sequence (tryInit/readConfig/add/contains/count/sizeInMemory/expire/renamenx/delete,
+    addAllAsync/mergeWithAsync/countWithAsync with the completion upcall)."""
+    exe = os.path.join(ROOT, "tests", "c", "_build", "ffm_replay")
+    assert os.path.exists(exe), "built by __graft_entry__.build() (make -C redisson_amd/csrc)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout

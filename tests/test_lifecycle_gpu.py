@@ -295,3 +295,17 @@ def test_element_partitioned_exchange_two_processes(fresh):
         p.join(timeout=240)
         assert p.exitcode == 0, p.exitcode
     assert list(result) == [1, 1]
+
+
+def test_size_in_memory(client, fresh):
+    """sizeInMemory (M/RedissonBloomFilter.java:234-238): the bitmap and the config hash; the
+    bitmap's share is its device allocation (bytes rounded to 256, plus the length-word tail)."""
+    f = client.getBloomFilter(fresh)
+    assert f.sizeInMemory() == 0
+    f.tryInit(1000, 0.01)  # 9585 bits -> 1199 bytes -> 1280 allocated
+    v0 = f.sizeInMemory()
+    assert v0 > 0
+    f.add(["a"])
+    assert f.sizeInMemory() - v0 == 1280 + 256 + len(fresh)
+    f.delete()
+    assert f.sizeInMemory() == 0

@@ -1,0 +1,153 @@
+"""One process over the GPUs of a node (rbx_node_*): slot routing, scatter / concurrent run /
+gather of multi-tenant batches, and cross-GPU PFCOUNT / PFMERGE -- per key against the oracle.
+
+The box has one GPU, so the node is rehearsed with several contexts on device 0 (devices =
+[0] * N): every context has its own keyspace, streams and scratch exactly as it would on its
+own GPU, and the routing is the one an 8-GPU node uses (slot * N / 16384,
+M/cluster/ClusterConnectionManager.java:777-830)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from redisson_amd import Arena, IllegalStateException, RedissonClient
+from redisson_amd import _lib as L
+from redisson_amd.node import RedissonNode
+
+pytestmark = pytest.mark.gpu
+N = 4
+
+
+@pytest.fixture(scope="module")
+def node():
+    nd = RedissonNode(N, devices=[0] * N)
+    yield nd
+    nd.shutdown()
+
+
+def test_routing_matches_calc_slot(node, fresh):
+    names = [f"{fresh}:{i}" for i in range(200)] + [f"{{{fresh}}}:{i}" for i in range(5)]
+    for nm in names:
+        assert node.gpu_of(nm) == O.calc_slot(nm.encode()) * N // 16384
+    # hashtags pin a group to one GPU; the config hash shares its filter's slot
+    assert len({node.gpu_of(f"{{{fresh}}}:{i}") for i in range(5)}) == 1
+    assert node.gpu_of(fresh) == node.gpu_of("{" + fresh + "}:config")
+
+
+def test_multitenant_batch_scatter_gather(node, fresh):
+    rng = np.random.default_rng(41)
+    T = 40
+    names = [f"{fresh}-tenant:{t:03d}" for t in range(T)]
+    gpus = {node.gpu_of(n) for n in names}
+    assert len(gpus) > 1  # the batch really spans contexts
+    ref = {}
+    for nm in names:
+        assert node.getBloomFilter(nm).tryInit(20_000, 0.01)
+        cfg = node.getBloomFilter(nm)
+        ref[nm] = O.OracleBloom(cfg.getSize(), cfg.getHashIterations())
+    per = rng.integers(1, 300, size=T)
+    seg = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
+    keys = [rng.bytes(int(L_)) for L_ in rng.integers(1, 48, size=int(seg[-1]))]
+    # add, per key flags and counts in segment order
+    counts, flags = node.bloom_add_multi(names, seg, Arena(keys), per_key=True)
+    for s, nm in enumerate(names):
+        c, f = ref[nm].add(*O.arena(keys[seg[s]:seg[s + 1]]), per_key=True)
+        assert counts[s] == c and np.array_equal(flags[seg[s]:seg[s + 1]], f), nm
+    # contains of the same keys plus fresh ones, repeated tenants in one batch (segment order)
+    order = list(range(T)) + [3, 3, 17]
+    ks, segs = [], [0]
+    for s in order:
+        ks += keys[seg[s]:seg[s + 1]] + [rng.bytes(20) for _ in range(50)]
+        segs.append(len(ks))
+    counts, pres = node.bloom_contains_multi([names[s] for s in order], segs, Arena(ks), per_key=True)
+    for j, s in enumerate(order):
+        c, p = ref[names[s]].contains(*O.arena(ks[segs[j]:segs[j + 1]]), per_key=True)
+        assert counts[j] == c and np.array_equal(pres[segs[j]:segs[j + 1]], p)
+    # each tenant lives only on its slot's context: its bitmap bytes equal the oracle's there
+    for nm in names[:8]:
+        g = node.gpu_of(nm)
+        import ctypes as C
+
+        ctx = C.c_void_p()
+        assert L.lib().rbx_node_ctx(node.node, g, C.byref(ctx)) == 0
+        n = C.c_uint64()
+        buf = np.zeros((abs(ref[nm].size) + 7) // 8 + 1, np.uint8)
+        assert L.lib().rbx_bloom_export(ctx, nm.encode(), buf.ctypes.data_as(L.u8p), buf.size, C.byref(n)) == 0
+        assert buf[: n.value].tobytes() == ref[nm].redis_string()
+        for other in range(N):
+            if other == g:
+                continue
+            assert L.lib().rbx_node_ctx(node.node, other, C.byref(ctx)) == 0
+            e = C.c_int()
+            assert L.lib().rbx_bloom_is_exists(ctx, nm.encode(), C.byref(e)) == 0 and e.value == 0
+    # fixed-stride arenas scatter too
+    mat = rng.integers(0, 256, size=(600, 16), dtype=np.uint8)
+    fseg = np.array([0, 100, 250, 600], np.uint64)
+    fcounts = node.bloom_contains_multi(names[:3], fseg, Arena.fixed(mat))
+    for s in range(3):
+        assert fcounts[s] == ref[names[s]].contains(*O.fixed_arena(mat[fseg[s]:fseg[s + 1]]))
+    assert node.delete(*names, *["{" + n + "}:config" for n in names]) == 2 * T
+
+
+def test_uninitialized_tenant_raises(node, fresh):
+    with pytest.raises(IllegalStateException):
+        node.bloom_contains_multi([fresh + "-x"], [0, 1], Arena([b"k"]))
+
+
+def test_config_recreated_with_other_parameters(node, fresh):
+    """A cached per-GPU handle whose config was re-created with other (size, k) is replaced: the
+    batch reads the new config like a freshly created RBloomFilter."""
+    nm = fresh + "-re"
+    keys = [b"a", b"b", b"c"]
+    f = node.getBloomFilter(nm)
+    f.tryInit(1000, 0.01)
+    assert node.bloom_add_multi([nm], [0, 3], Arena(keys))[0] == 3
+    node.delete(nm, "{" + nm + "}:config")
+    f.tryInit(5000, 0.001)
+    ref = O.OracleBloom(*O.bloom_optimal(5000, 0.001))
+    assert node.bloom_add_multi([nm], [0, 3], Arena(keys))[0] == ref.add(*O.arena(keys))
+    node.delete(nm, "{" + nm + "}:config")
+
+
+def test_node_hll_routing_and_cross_gpu_union(node, fresh):
+    rng = np.random.default_rng(42)
+    names = [f"{fresh}-h{i}" for i in range(12)]
+    assert len({node.gpu_of(n) for n in names}) > 1
+    mats = [rng.integers(0, 256, size=(int(rng.integers(100, 4000)), 16), dtype=np.uint8) for _ in names]
+    seg = np.concatenate([[0], np.cumsum([m.shape[0] for m in mats])]).astype(np.uint64)
+    allm = np.concatenate(mats)
+    ch = node.hll_add_multi(names, seg, Arena.fixed(allm))
+    assert ch.tolist() == [1] * len(names)
+    regs = []
+    for m in mats:
+        r = O.hll_new()
+        O.hll_pfadd(r, *O.fixed_arena(m))
+        regs.append(r)
+    for nm, r in zip(names, regs):
+        assert node.getHyperLogLog(nm).count() == O.hll_count(r)
+    # PFCOUNT over names on different GPUs = count of the union
+    u = O.hll_new()
+    for r in regs:
+        O.hll_merge(u, r)
+    assert node.getHyperLogLog(names[0]).countWith(*names[1:]) == O.hll_count(u)
+    # PFMERGE into a destination on yet another slot
+    dest = fresh + "-dest"
+    node.getHyperLogLog(dest).mergeWith(*names)
+    assert node.getHyperLogLog(dest).count() == O.hll_count(u)
+    # the staged temporaries are gone: only the test's keys remain
+    assert node.delete(*names, dest) == len(names) + 1
+
+
+def test_node_and_single_context_agree(node, fresh):
+    """The same single-tenant calls through the node and through one plain context."""
+    rng = np.random.default_rng(43)
+    keys = [rng.bytes(24) for _ in range(5000)]
+    nf = node.getBloomFilter(fresh)
+    nf.tryInit(10_000, 0.01)
+    with RedissonClient(0) as c:
+        cf = c.getBloomFilter(fresh)
+        cf.tryInit(10_000, 0.01)
+        assert nf.add(keys) == cf.add(keys)
+        probe = keys[:2000] + [rng.bytes(24) for _ in range(2000)]
+        assert nf.containsEach(probe)[1].tolist() == cf.containsEach(probe)[1].tolist()
+        assert nf.count() == cf.count()
+    node.delete(fresh, "{" + fresh + "}:config")
