@@ -17,6 +17,11 @@ int rbx_bench_gather(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, ui
  * region_bytes-sized regions assigned round-robin by blockIdx % 8 (XCD affinity). */
 int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, uint64_t region_bytes,
                              uint64_t nlanes, unsigned grid, void *d_sink, void *stream);
+/* Slice-probe roofline: nbuckets buckets of per_bucket 8-byte entries {word offset, payload}
+ * (device, [bucket][per_bucket]); bucket b's entries each test one word of the bitmap slice
+ * b * slice_bytes (a power of two); workgroups take buckets by blockIdx % 8 (XCD affinity). */
+int rbx_bench_slice_probe(rbx_ctx *ctx, const void *d_entries, uint64_t per_bucket, uint32_t nbuckets,
+                          const void *d_bitmap, uint64_t slice_bytes, unsigned grid, void *d_sink, void *stream);
 /* Stream-read roofline probe: reads `bytes` (16-byte aligned buffer) with 16-byte loads. */
 int rbx_bench_stream_read(rbx_ctx *ctx, const void *d_buf, uint64_t bytes, void *d_sink, void *stream);
 /* Segment-local gather probe (the locality of a multi-tenant batch): key i belongs to segment

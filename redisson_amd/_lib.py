@@ -165,6 +165,7 @@ SIGNATURES = {
     "rbx_node_hll_add_multi": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
     "rbx_node_hll_count": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p]),
     "rbx_node_hll_merge": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
+    "rbx_bench_slice_probe": (C.c_int, [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint, vp, vp]),
     "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
     "rbx_bench_gather_segments": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp]),
     # binary names (rbx_name)

@@ -1432,6 +1432,42 @@ void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStre
     hipLaunchKernelGGL(k_stream_read, dim3(4096), dim3(256), 0, st, (const u32x4 *)buf, bytes / 16, sink);
 }
 
+// Slice-probe roofline: the bitmap is cut into nbuckets slices of 2^slice_log2 bytes; bucket b's
+// entries (8 bytes: word offset in the slice, payload) are streamed and each tests one word of
+// slice b.  Workgroup w takes the buckets w % 8, w % 8 + 8, ... (blocks b and b + 8 share an XCD
+// under the observed round-robin placement: speed only), so one XCD's workgroups gather inside
+// one slice at a time and the slice can stay in that XCD's L2.
+__global__ __launch_bounds__(256) void k_bench_slice_probe(const u32x2 *__restrict__ ent, uint64_t per_bucket,
+                                                           uint32_t nbuckets, const uint32_t *__restrict__ bm,
+                                                           uint32_t slice_words_log2, uint32_t *__restrict__ sink) {
+    const uint32_t x = blockIdx.x & 7, local = blockIdx.x >> 3, nlocal = gridDim.x >> 3;
+    uint32_t acc = 0;
+    for (uint32_t b = x; b < nbuckets; b += 8) {
+        const u32x2 *e = ent + (uint64_t)b * per_bucket;
+        const uint32_t *slice = bm + ((uint64_t)b << slice_words_log2);
+        const uint64_t step = (uint64_t)nlocal * 256;
+        uint64_t i = (uint64_t)local * 256 + threadIdx.x;
+        for (; i + 3 * step < per_bucket; i += 4 * step) {
+            u32x2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(e + i + u * step);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc ^= slice[v[u].x & ((1u << slice_words_log2) - 1)] ^ v[u].y;
+        }
+        for (; i < per_bucket; i += step) {
+            const u32x2 v = e[i];
+            acc ^= slice[v.x & ((1u << slice_words_log2) - 1)] ^ v.y;
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+void launch_bench_slice_probe(const void *ent, uint64_t per_bucket, uint32_t nbuckets, const uint32_t *bm,
+                              uint32_t slice_words_log2, unsigned grid, uint32_t *sink, hipStream_t st) {
+    hipLaunchKernelGGL(k_bench_slice_probe, dim3(grid), dim3(256), 0, st, (const u32x2 *)ent, per_bucket, nbuckets, bm,
+                       slice_words_log2, sink);
+}
+
 void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
                            uint32_t *sink, hipStream_t st, unsigned grid) {
     const uint64_t nregions = nwords / region_words;

@@ -525,10 +525,16 @@ static void bk_emit2(const PcArgs &a, hipStream_t st) {
                        a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
 }
 
+// EXPERIMENTS (rbx_tune "contains_emit2_nt"): emit2 workgroup size.  1024 threads hold 96 KiB of
+// LDS (one block per CU); 512 threads hold 67 KiB (two blocks per CU).
+static int g_emit2_nt = 1024;
+void set_contains_emit2_nt(int v) { g_emit2_nt = v; }
+
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
     bk_stage1<KLEN, KMAX, 512>(a, st);
-    bk_emit2<1024>(a, st);
+    if (g_emit2_nt == 512) bk_emit2<512>(a, st);
+    else bk_emit2<1024>(a, st);
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
                        a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges, a.flags);
     hipLaunchKernelGGL(k_bk_misses, dim3(2048), dim3(1024), 0, st, a.mrec, a.mcnt, a.capm, a.nmranges, a.miss);

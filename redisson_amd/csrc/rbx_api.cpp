@@ -2407,6 +2407,19 @@ int rbx_bench_gather(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint
     return RBX_OK;
 }
 
+int rbx_bench_slice_probe(rbx_ctx *c, const void *d_entries, uint64_t per_bucket, uint32_t nbuckets,
+                          const void *d_bitmap, uint64_t slice_bytes, unsigned grid, void *d_sink, void *stream) {
+    if (!c || !d_entries || !d_bitmap || !d_sink || grid < 8 || slice_bytes < 4 || (slice_bytes & (slice_bytes - 1)))
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    RBX_TRY(set_device(c));
+    uint32_t lg = 0;
+    while ((4ULL << lg) < slice_bytes) ++lg;
+    launch_bench_slice_probe(d_entries, per_bucket, nbuckets, (const uint32_t *)d_bitmap, lg, grid & ~7u,
+                             (uint32_t *)d_sink, pick_stream(c, stream));
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
 int rbx_bench_stream_read(rbx_ctx *c, const void *d_buf, uint64_t bytes, void *d_sink, void *stream) {
     if (!c || !d_buf || !d_sink || ((uintptr_t)d_buf & 15)) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
     RBX_TRY(set_device(c));
@@ -2568,6 +2581,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "contains_qgrid")) {
         if (value < 256 || value > 8192) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qgrid in [256, 8192]");
         set_contains_qgrid(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "contains_emit2_nt")) {
+        if (value != 512 && value != 1024) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024}");
+        set_contains_emit2_nt(value);
         return RBX_OK;
     }
     if (!strcmp(key, "contains_stage1")) {

@@ -86,6 +86,7 @@ inline unsigned grid_for_pc(uint64_t n) {
     return (unsigned)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 }
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
+void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 constexpr int kBaRegionBits = 15;               // 32K-bit regions: owner array (128 KiB) + bitmap (4 KiB) in LDS
@@ -149,6 +150,9 @@ void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region
 // one seg_words slice): the request roofline of multi-tenant batches at their locality
 void launch_gather_segments(const uint32_t *tbl, uint64_t nwords, uint64_t seg_words, uint64_t keys_per_seg,
                             uint64_t nkeys, uint32_t *sink, hipStream_t st);
+// slice-probe roofline: per bucket b, stream 8-byte entries and test one word of bitmap slice b
+void launch_bench_slice_probe(const void *ent, uint64_t per_bucket, uint32_t nbuckets, const uint32_t *bm,
+                              uint32_t slice_words_log2, unsigned grid, uint32_t *sink, hipStream_t st);
 // streaming 16-byte reads of a whole buffer: the HBM stream-read roofline probe
 void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStream_t st);
 // random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe

@@ -74,6 +74,31 @@ def main():
                                   "gathers_per_s": lanes * 6 / (ms / 1e3)}), flush=True)
         del tb
 
+    if "slices" in a.what:
+        # the L2-sliced probe: 324M 8-byte entries (C2's survivor pairs) bucketed by bitmap slice,
+        # each testing one word of its slice; vs the random gather over the whole 512 MiB
+        bm = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+        bm.random_(0, 255, generator=g)
+        total = 324_000_000
+        ent = torch.randint(0, 2**31 - 1, (total * 2,), dtype=torch.int32, device="cuda", generator=g)
+        for slice_mb in [1, 2, 4, 8]:
+            nb = (512 << 20) // (slice_mb << 20)
+            per = total // nb
+            for grid in [2048, 4096, 8192]:
+                f = lambda: L.lib().rbx_bench_slice_probe(client.ctx, ent.data_ptr(), per, nb, bm.data_ptr(),
+                                                          slice_mb << 20, grid, sink.data_ptr(), sp)
+                f()
+                ms = timed(stream, f, 5)
+                print(json.dumps({"bench": "slice_probe", "slice_MiB": slice_mb, "grid": grid, "entries": per * nb,
+                                  "ms": ms, "entries_per_s": per * nb / (ms / 1e3),
+                                  "stream_GBps": per * nb * 8 / (ms / 1e3) / 1e9}), flush=True)
+        f = lambda: L.lib().rbx_bench_gather(client.ctx, bm.data_ptr(), bm.numel(), total // 7, 7, sink.data_ptr(), sp)
+        f()
+        ms = timed(stream, f, 3)
+        print(json.dumps({"bench": "gather_512MiB", "gathers": total, "ms": ms, "gathers_per_s": total / (ms / 1e3)}),
+              flush=True)
+        del ent, bm
+
     if "hostpath" in a.what:
         import ctypes as C
         import time as T
