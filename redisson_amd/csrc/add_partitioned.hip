@@ -33,7 +33,7 @@ __device__ __forceinline__ void ba_write_run(const unsigned long long *s_img, ui
                                              uint32_t *__restrict__ overflow) {
     for (uint32_t t = lane; t < n; t += 64) {
         const uint64_t gp = gb + t;
-        if (gp < cap) __builtin_nontemporal_store(s_img[st + t], dst + gp);
+        if (gp < cap) run_store(s_img[st + t], dst + gp);
         else *overflow = 1u;
     }
 }
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(1024) void k_ba_region(const unsigned long long *__
         for (uint32_t q = wave; q < nranges; q += NT / 64) {
             const uint32_t rn = s_rc[q], st = s_rstart[q];
             uint32_t *dst = recs + (uint64_t)q * cap_rec + s_rgb[q];
-            for (uint32_t t = lane; t < rn; t += 64) __builtin_nontemporal_store(s_rec[st + t], dst + t);
+            for (uint32_t t = lane; t < rn; t += 64) run_store(s_rec[st + t], dst + t);
         }
         __syncthreads();
     }

@@ -6,6 +6,17 @@
 
 namespace rbx {
 
+// Stores of the partition passes' runs.  Experiment builds (-DRBX_RUN_STORES_PLAIN, tools/_ab/)
+// use plain stores instead, which keep the line in the XCD's L2 where partial lines written by
+// different workgroups can merge before write-back.
+template <class T> __device__ __forceinline__ void run_store(T v, T *p) {
+#ifdef RBX_RUN_STORES_PLAIN
+    *p = v;
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+}
+
 // HighwayHash128 of key i (Hash.hash128, M/misc/Hash.java:53-74): 16/32/64-byte fast path or
 // the generic any-length path
 template <int KLEN>

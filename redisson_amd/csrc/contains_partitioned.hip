@@ -54,9 +54,9 @@ __device__ __forceinline__ void bk_put6(unsigned long long e, uint64_t gp, uint3
                                         unsigned long long *__restrict__ miss) {
     if (gp < cap) {
         const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
-        __builtin_nontemporal_store(((idx & ((1u << kBkRegionBits) - 1)) << kBkKeyLoBits) |
+        run_store(((idx & ((1u << kBkRegionBits) - 1)) << kBkKeyLoBits) |
                                         (key & ((1u << kBkKeyLoBits) - 1)), lo + gp);
-        __builtin_nontemporal_store((uint16_t)(key >> kBkKeyLoBits), hi + gp);
+        run_store((uint16_t)(key >> kBkKeyLoBits), hi + gp);
     } else {
         bk_direct(e, bm, miss);
     }
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
             const uint64_t room = cap1 - min<uint64_t>(cap1, s_gb[b]);
             for (uint32_t t = lane; t < full; t += 64) {  // carried pairs first, then this tile's run
                 const unsigned long long e = t < cn ? s_car[b * kBkLine1 + t] : s_img[st + t - cn];
-                if (t < room) __builtin_nontemporal_store(e, dst + t);
+                if (t < room) run_store(e, dst + t);
                 else bk_direct(e, bm, miss);
             }
             if (full == 0) {  // cn + n < one line: append the run to the carry
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         if (lane < kBkLine1) {
             const unsigned long long e = s_car[b * kBkLine1 + min(lane, cn - 1)];
             if ((uint64_t)gb + lane < cap1)
-                __builtin_nontemporal_store(e, pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + gb + lane);
+                run_store(e, pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + gb + lane);
             else bk_direct(e, bm, miss);
         }
     }
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                 const uint64_t gb = s_mgb[q];
                 for (uint32_t t = lane; t < cq; t += 64) {
                     const uint32_t key = s_mimg[st + t];
-                    if (gb + t < capm) __builtin_nontemporal_store(key, mrec + (uint64_t)q * capm + gb + t);
+                    if (gb + t < capm) run_store(key, mrec + (uint64_t)q * capm + gb + t);
                     else bk_miss_direct(key, miss);
                 }
             }

@@ -194,6 +194,77 @@ void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipSt
 }
 
 // ---------------------------------------------------------------------------------
+// sparse-limit check (one block per HLL): would the registers still fit Redis' sparse string?
+// Bytes of the fewest-bytes opcode form: a zero run costs 1 byte (ZERO, <= 64) or 2 (XZERO), a
+// run of value v <= 32 costs ceil(len / 4) bytes (VAL); a register > 32 forces dense.  Thread t
+// owns registers [64t, 64t + 64); a run is charged by the thread holding its first register,
+// which finds the run's end through a suffix minimum of the threads' first run starts.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hll_sparse_check(const HllCheck *__restrict__ items, uint64_t max_bytes) {
+    const HllCheck it = items[blockIdx.x];
+    __shared__ uint32_t s_first[257];
+    __shared__ uint32_t s_sum[4], s_max[4];
+    if (__hip_atomic_load(it.promoted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // sticky, uniform
+    const uint32_t t = threadIdx.x, base = t * 64;
+    uint8_t r[64];
+    const u8x16 *src = (const u8x16 *)(it.regs + base);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const u8x16 v = src[q];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r[q * 16 + j] = v[j];
+    }
+    const uint32_t prev = t ? it.regs[base - 1] : 0xffffffffu;
+    uint64_t starts = 0;
+    uint32_t vmax = 0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        const uint32_t p = j ? (uint32_t)r[j - 1] : prev;
+        if (r[j] != p) starts |= 1ULL << j;
+        vmax = r[j] > vmax ? r[j] : vmax;
+    }
+    s_first[t] = starts ? base + (uint32_t)__builtin_ctzll(starts) : 16384u;
+    if (t == 0) s_first[256] = 16384u;
+    __syncthreads();
+    // suffix minimum over the threads' first starts (256 entries, in place)
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        const uint32_t o = t + off < 256 ? s_first[t + off] : 16384u;
+        __syncthreads();
+        s_first[t] = min(s_first[t], o);
+        __syncthreads();
+    }
+    const uint32_t next_after = t + 1 < 256 ? s_first[t + 1] : 16384u;  // first start past my range
+    uint32_t bytes = 0;
+    for (uint64_t m = starts; m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint64_t later = m & (m - 1);
+        const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
+        const uint32_t len = end - (base + j), v = r[j];
+        bytes += v == 0 ? (len > 64 ? 2u : 1u) : (len + 3) / 4;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        bytes += __shfl_down(bytes, off, 64);
+        vmax = max(vmax, (uint32_t)__shfl_down(vmax, off, 64));
+    }
+    if ((t & 63) == 0) {
+        s_sum[t >> 6] = bytes;
+        s_max[t >> 6] = vmax;
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+        const uint32_t mx = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+        if (mx > 32 || 16 + (uint64_t)total > max_bytes) *it.promoted = 1u;
+    }
+}
+
+void launch_hll_sparse_check(const HllCheck *items, uint32_t n, uint64_t max_bytes, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_hll_sparse_check, dim3(n), dim3(256), 0, st, items, max_bytes);
+}
+
+// ---------------------------------------------------------------------------------
 // register exchange: HLL i <-> buf[i * 16384 ..], one block per HLL, 16 B per lane
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_hll_pack(uint8_t *const *__restrict__ regs, uint8_t *__restrict__ buf,

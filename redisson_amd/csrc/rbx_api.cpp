@@ -130,6 +130,7 @@ struct Bitmap {  // a Redis string used with SETBIT/GETBIT
 
 struct HllState {  // a Redis HLL string, registers unpacked (1 byte each) on the device
     uint8_t *d_regs = nullptr;  // 16384 bytes inside a pool chunk
+    uint32_t *d_promoted = nullptr;  // device word: a PFADD made the sparse string exceed its limits
     uint64_t card = 0;          // the header's 8 cached-cardinality bytes (LE); bit 63 = invalid
     bool dense = false;         // Redis encoding: created sparse, promoted to dense once (never back)
     struct ::rbx_ctx *owner = nullptr;
@@ -193,7 +194,9 @@ struct rbx_ctx {
 
     // HLL register pool: chunks of kHllPerChunk x 16 KiB
     std::vector<uint8_t *> hll_chunks;
-    std::vector<uint8_t *> hll_free;
+    std::vector<std::pair<uint8_t *, uint32_t *>> hll_free;  // (registers, promotion word)
+    DevBuf hll_checks;                     // k_hll_sparse_check items (cached by content)
+    std::vector<HllCheck> check_cache;
 
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -245,7 +248,7 @@ rbx::HllState::~HllState() {
     if (d_regs && owner) {
         {
             std::lock_guard<std::recursive_mutex> g(owner->ks.mu);
-            if (!owner->shut) owner->hll_free.push_back(d_regs);
+            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted});
         }
         ctx_release(owner);
     }
@@ -254,18 +257,22 @@ rbx::HllState::~HllState() {
 // A fresh zeroed HLL register block; the fill runs on `st` (see SlabPool).
 static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out) {
     if (c->hll_free.empty()) {
+        // registers of kHllPerChunk HLLs, then their promotion words
         uint8_t *chunk = nullptr;
-        HIP_TRY(hipMalloc(&chunk, kHllBytes * kHllPerChunk));
+        HIP_TRY(hipMalloc(&chunk, (kHllBytes + 4) * kHllPerChunk));
         c->hll_chunks.push_back(chunk);
+        uint32_t *words = (uint32_t *)(chunk + kHllBytes * kHllPerChunk);
         // hand out in reverse so that successive allocations are ascending
-        for (size_t i = kHllPerChunk; i-- > 0;) c->hll_free.push_back(chunk + i * kHllBytes);
+        for (size_t i = kHllPerChunk; i-- > 0;) c->hll_free.push_back({chunk + i * kHllBytes, words + i});
     }
     auto h = std::make_shared<HllState>();
-    h->d_regs = c->hll_free.back();
+    h->d_regs = c->hll_free.back().first;
+    h->d_promoted = c->hll_free.back().second;
     c->hll_free.pop_back();
     h->owner = c;
     c->refs.fetch_add(1);
     HIP_TRY(hipMemsetAsync(h->d_regs, 0, kHllBytes, st));
+    HIP_TRY(hipMemsetAsync(h->d_promoted, 0, 4, st));
     *out = h;
     return RBX_OK;
 }
@@ -1513,6 +1520,7 @@ int rbx_bloom_add_multi(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, co
 
 // ---- HyperLogLog ------------------------------------------------------------------------------
 static constexpr uint64_t kTileElems = 65536;  // elements per PFADD workgroup
+constexpr uint64_t kHllSparseMaxBytes = 3000;  // redis.conf hll-sparse-max-bytes (default)
 
 static const char *kHllWrongType = "WRONGTYPE Key is not a valid HyperLogLog string value.";
 
@@ -1553,6 +1561,44 @@ static int hll_bind(rbx_ctx *c, rbx_hll *h, bool create, hipStream_t st) {
     return RBX_OK;
 }
 
+// Redis promotes a sparse HLL to dense (one way) when an update would store a value > 32 or grow
+// the sparse string past hll-sparse-max-bytes ([redis-7.2] hyperloglog.c hllSparseSet).  After
+// every PFADD command (and PFMERGE into a sparse destination) k_hll_sparse_check sets the HLL's
+// sticky device word when its registers no longer fit; RBX_HLL_AS_STORED export and PFMERGE read
+// it.  (Redis checks after every element; the sparse length is not monotone -- runs can merge --
+// so a string that exceeded the limit mid-command and shrank again by its end stays sparse here:
+// parity unpinned without a live redis-server.)
+static int sparse_check(rbx_ctx *c, const std::vector<HllState *> &hl, hipStream_t st) {
+    std::vector<HllCheck> items;
+    std::unordered_map<HllState *, int> seen;
+    for (HllState *h : hl)
+        if (h && !h->dense && !seen.count(h)) {
+            seen[h] = 1;
+            items.push_back(HllCheck{h->d_regs, h->d_promoted});
+        }
+    if (items.empty()) return RBX_OK;
+    const bool same = c->check_cache.size() == items.size() &&
+                      memcmp(c->check_cache.data(), items.data(), items.size() * sizeof(HllCheck)) == 0;
+    if (!same) {
+        RBX_TRY(c->hll_checks.reserve(items.size() * sizeof(HllCheck)));
+        HIP_TRY(hipMemcpyAsync(c->hll_checks.p, items.data(), items.size() * sizeof(HllCheck), hipMemcpyHostToDevice, st));
+        c->check_cache = items;
+    }
+    launch_hll_sparse_check(c->hll_checks.as<HllCheck>(), (uint32_t)items.size(), kHllSparseMaxBytes, st);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+// host view of the promotion word (the caller holds a ScratchOrder on c->stream)
+static int resolve_dense(rbx_ctx *c, HllState *h) {
+    if (h->dense) return RBX_OK;
+    uint32_t w = 0;
+    HIP_TRY(hipMemcpyAsync(&w, h->d_promoted, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (w) h->dense = true;
+    return RBX_OK;
+}
+
 // PFADD batch: device elements, commands in order.  Commands naming the same HLL are
 // split into successive launches so each reply sees the previous commands' effect.
 static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64_t *h_seg, const KeysDev &dk,
@@ -1586,6 +1632,8 @@ static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64
             }
             launch_hll_pfadd(dk, fl, c->hll_tiles.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
             HIP_TRY(hipGetLastError());
+            std::vector<HllState *> round(hl.begin() + s0, hl.begin() + s1);
+            RBX_TRY(sparse_check(c, round, st));
         }
         s0 = s1;
     }
@@ -1853,12 +1901,17 @@ static int hll_merge(rbx_ctx *c, const std::string &dest, const std::vector<std:
     }
     std::shared_ptr<HllState> d;
     RBX_TRY(hll_get(c, dest, true, c->stream, &d, nullptr));
-    for (auto &h : keep) d->dense = d->dense || h->dense;  // pfmergeCommand: use_dense if any input is
+    RBX_TRY(resolve_dense(c, d.get()));
+    for (auto &h : keep) {
+        RBX_TRY(resolve_dense(c, h.get()));
+        d->dense = d->dense || h->dense;  // pfmergeCommand: use_dense if any input is
+    }
     if (!sp.empty()) {
         RBX_TRY(c->ptrs.reserve(sp.size() * sizeof(uint8_t *)));
         HIP_TRY(hipMemcpyAsync(c->ptrs.p, sp.data(), sp.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
         launch_hll_merge(d->d_regs, c->ptrs.as<uint8_t *>(), (uint32_t)sp.size(), c->stream);
         HIP_TRY(hipGetLastError());
+        RBX_TRY(sparse_check(c, {d.get()}, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
@@ -1882,7 +1935,6 @@ int rbx_hll_merge_n(rbx_ctx *c, rbx_name dest, const rbx_name *srcs, uint32_t ns
 // Redis HLL strings: 16-byte header ("HYLL", encoding, 3 unused, 8 cached-cardinality bytes)
 // + dense registers (HLL_DENSE_SET_REGISTER layout, 6 bits each, LSB-first) or sparse opcodes.
 constexpr uint64_t kHllDenseLen = 16 + 12288;
-constexpr uint64_t kHllSparseMaxBytes = 3000;  // redis.conf hll-sparse-max-bytes (default)
 
 static void hll_header(uint8_t *s, int sparse, uint64_t card) {
     memcpy(s, "HYLL", 4);
@@ -1942,6 +1994,7 @@ static int hll_export_enc(rbx_ctx *c, const std::string &name, int encoding, uin
         if (len) *len = 0;
         return RBX_OK;
     }
+    if (encoding == RBX_HLL_AS_STORED) RBX_TRY(resolve_dense(c, h.get()));
     std::vector<uint8_t> regs(kHllBytes);
     HIP_TRY(hipMemcpyAsync(regs.data(), h->d_regs, kHllBytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2039,6 +2092,7 @@ static int hll_import(rbx_ctx *c, const std::string &name, const uint8_t *bytes,
     for (int i = 0; i < 8; ++i) card |= (uint64_t)bytes[8 + i] << (8 * i);
     h->card = card;
     h->dense = bytes[4] == 0;  // SET keeps the string's encoding
+    HIP_TRY(hipMemsetAsync(h->d_promoted, 0, 4, c->stream));
     HIP_TRY(hipMemcpyAsync(h->d_regs, regs.data(), kHllBytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RBX_OK;

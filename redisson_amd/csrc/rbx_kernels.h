@@ -183,6 +183,12 @@ void launch_hll_count(uint8_t *const *d_regs, uint32_t n, int *d_histo, unsigned
 void launch_hll_merge(uint8_t *dst, uint8_t *const *d_srcs, uint32_t nsrc, hipStream_t st);
 // raw registers -> scratch union: out = max over a set of HLLs (multi-key PFCOUNT)
 void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipStream_t st);
+struct HllCheck {
+    uint8_t *regs;
+    uint32_t *promoted;  // sticky: set when the registers no longer fit a sparse string
+};
+// per item: promoted |= (a register > 32 || 16 + sparse opcode bytes > max_bytes)
+void launch_hll_sparse_check(const HllCheck *items, uint32_t n, uint64_t max_bytes, hipStream_t st);
 // buf[i*16384..] = regs[i] (pack) or regs[i] = max(regs[i], buf[i*16384..]) (unpack_max)
 void launch_hll_pack(uint8_t *const *d_regs, uint32_t n, uint8_t *buf, bool unpack_max, hipStream_t st);
 

@@ -314,3 +314,41 @@ def test_large_batch_accuracy_and_parity(client, fresh):
         assert counts[i] == O.hll_count(r)
         assert np.array_equal(regs_of(client.getHyperLogLog(names[i])), r)
     assert np.all(np.abs(counts.astype(np.float64) - per) / per < 0.03)
+
+
+def _count1_elements(indexes, rng):
+    """One 16-byte element per target register index whose MurmurHash64A gives that index and
+    count 1 (bit 14 of the hash set: hllPatLen = 1)."""
+    want = set(int(i) for i in indexes)
+    found = {}
+    while len(found) < len(want):
+        cand = rng.integers(0, 256, size=(1 << 20, 16), dtype=np.uint8)
+        h = O.murmur_batch(*O.fixed_arena(cand))
+        idx = (h & np.uint64(16383)).astype(np.int64)
+        ok = ((h >> np.uint64(14)) & np.uint64(1)) == 1
+        for j in np.nonzero(ok)[0]:
+            i = int(idx[j])
+            if i in want and i not in found:
+                found[i] = bytes(cand[j])
+    return [found[i] for i in sorted(want)]
+
+
+def test_sparse_promotion_is_checked_per_command(client, fresh):
+    """Redis promotes during the PFADD that first overflows hll-sparse-max-bytes, even if a later
+    PFADD shrinks the sparse form again (merging runs).  Command 1 sets every even register of
+    [0, 8000) to 1: 4000 VAL + 4000 ZERO opcodes, > 3000 bytes -> promoted.  Command 2 fills the
+    odd ones: the fewest-bytes form of the final registers (2000 VAL opcodes) would fit, but the
+    key stays dense (promotion is one way)."""
+    rng = np.random.default_rng(61)
+    even = _count1_elements(range(0, 8000, 2), rng)
+    odd = _count1_elements(range(1, 8000, 2), rng)
+    h = client.getHyperLogLog(fresh)
+    assert h.addAll(Arena(even))
+    assert h.addAll(Arena(odd))
+    regs = O.hll_new()
+    regs[:8000] = 1
+    s = h.exportString()  # as stored
+    assert s[4] == 0 and np.array_equal(O.hll_dense_unpack(s[16:]), regs)
+    ops = O.hll_sparse_pack(regs)
+    assert 16 + len(ops) <= 3000  # what an export-time check would have kept sparse
+    h.delete()
