@@ -178,7 +178,7 @@ struct rbx_ctx {
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
-    DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits;  // partitioned add
+    DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits, pa_ctr;  // partitioned add
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     DevBuf hll_pack;                                // contiguous registers for the RCCL merge
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
@@ -495,6 +495,7 @@ static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_fi
 // the first-setter table at every size from 8 MiB to 512 MiB: tools/microbench.py psizes).
 static int g_add_partition_mode = 2;
 static int g_add_partition_diag = 0;
+static int g_add_record_policy = 2;
 
 static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << kBaRegionBits)) return false;
@@ -542,11 +543,17 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     const uint64_t b1 = (uint64_t)ncoarse * kBkSub * cap1 * 8, b3 = (uint64_t)nregions * cap3 * 8;
     RBX_TRY(c->pa_p1.reserve(std::max(b1, b3)));  // level 3 reuses level 1's buffer (consumed by level 2)
     RBX_TRY(c->pa_p2.reserve((uint64_t)n2 * cap2 * 8));
-    const uint64_t ncnt = 64 * kBkSub + n2 + nregions + nranges + 1;
+    const uint64_t ncnt = 64 * kBkSub + n2 + nregions + nranges + 2;
     RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
     RBX_TRY(c->pa_recs.reserve((uint64_t)nranges * cap_rec * 4));
     const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);
     RBX_TRY(c->pa_bits.reserve(nbw * 4));
+    // per-key non-owner counters (one byte per key; k_ba_keys zeroes what it read): zeroed once
+    // when (re)allocated
+    if (c->pa_ctr.cap < ((uint64_t)nranges << kBaKeyRangeBits)) {
+        RBX_TRY(c->pa_ctr.reserve((uint64_t)nranges << kBaKeyRangeBits));
+        HIP_TRY(hipMemsetAsync(c->pa_ctr.p, 0, c->pa_ctr.cap, st));
+    }
     const int fl = fast_len(keys);
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         BaArgs a{};
@@ -574,9 +581,12 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.cnt3 = a.cnt2 + n2;
         a.rec_cnt = a.cnt3 + nregions;
         a.overflow = a.rec_cnt + nranges;
+        a.mode = a.overflow + 1;
+        a.record_policy = (uint32_t)g_add_record_policy;
         a.recs = c->pa_recs.as<uint32_t>();
         a.nranges = (uint32_t)((a.nchunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
         a.new_bits = c->pa_bits.as<uint32_t>();
+        a.ctr = c->pa_ctr.as<uint32_t>();
         a.nwords4 = (size + 127) / 128 * 4;
         a.out_new = d_out_new;
         a.count = d_count;
@@ -777,7 +787,7 @@ int rbx_shutdown(rbx_ctx *c) {
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
                           &c->counters, &c->filt_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
-                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_recs, &c->pa_bits, &c->st_adds,
+                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_recs, &c->pa_bits, &c->pa_ctr, &c->st_adds,
                           &c->st_prefilter, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1]}) {
             if (b->p) (void)hipFree(b->p);
@@ -2604,10 +2614,20 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     // DIAGNOSTICS ONLY (tools/microbench.py padiag), results become wrong: 4 = the region kernel
-    // emits no records.  0 = normal.
+    // emits no records, 8 = it loads only its first two regions' pairs (compute floor), 16 = it
+    // only loads (load floor).  0 = normal.
     if (!strcmp(key, "add_partition_diag")) {
-        if (value != 0 && value != 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag in {0, 4}");
+        if (value < 0 || (value & ~28) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag: bits of 4|8|16");
         g_add_partition_diag = value;
+        return RBX_OK;
+    }
+    // How the add's region kernel reports which keys are new (add_partitioned.hip k_ba_mode):
+    // 0 owner records, 1 non-owner records, 3 non-owner counters, 2 (default) chosen from the
+    // sampled fill (< 1/16: counters, < 1/2: non-owner records, else owner records).  Exact
+    // either way.
+    if (!strcmp(key, "add_records")) {
+        if (value < 0 || value > 3) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_records in [0, 3]");
+        g_add_record_policy = value;
         return RBX_OK;
     }
     if (!strcmp(key, "add_partition")) {

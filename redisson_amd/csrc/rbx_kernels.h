@@ -89,9 +89,13 @@ void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream
 void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
-constexpr int kBaRegionBits = 15;               // 32K-bit regions: owner array (128 KiB) + bitmap (4 KiB) in LDS
+#ifndef RBX_BA_REGION_BITS
+#define RBX_BA_REGION_BITS 15
+#endif
+// 2^15-bit regions: owner array (128 KiB) + bitmap (4 KiB) in LDS (14: 64 KiB + 2 KiB, two blocks per CU)
+constexpr int kBaRegionBits = RBX_BA_REGION_BITS;
 constexpr int kBaKeyRangeBits = 20;             // records bucketed by 2^20-key ranges (128 KiB LDS bitmap)
-constexpr uint32_t kBaMaxRegionPairs = 6144;    // LDS record image: cap3 <= this
+constexpr uint32_t kBaMaxRegionPairs = 6144u >> (15 - kBaRegionBits);  // LDS record image: cap3 <= this
 struct BaArgs {
     KeysDev keys;
     uint64_t base, nchunk;
@@ -107,6 +111,9 @@ struct BaArgs {
     uint32_t nranges;
     uint32_t *new_bits;           // nranges x 2^15 words, zeroed per chunk
     uint32_t *overflow;           // zeroed; set when a pair does not fit (the chunk then reruns on the table path)
+    uint32_t *mode;               // written by k_ba_mode: 0 owner records, 1 non-owner records, 2 non-owner counters
+    uint32_t record_policy;       // rbx_tune "add_records": 0, 1, 3 = force mode 0, 1, 2; 2 = from the sampled fill
+    uint32_t *ctr;                // nranges x 2^20 byte counters (mode 2), all zero between calls
     uint64_t nwords4;             // bitmap words rounded up to a multiple of 4
     uint8_t *out_new;
     unsigned long long *count;

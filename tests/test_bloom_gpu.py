@@ -744,14 +744,16 @@ def test_pinned_host_arena(client, fresh):
         L_.lib().rbx_host_free(p)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode,records", [(0, 2), (1, 2), (1, 0), (1, 1), (1, 3)])
 @pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
                                       ((1 << 29) + 3, 16, 0), (1 << 20, 3, 24), (100_003, 2, 64)])
-def test_partitioned_add_parity(client, fresh, mode, size, k, L):
+def test_partitioned_add_parity(client, fresh, mode, records, size, k, L):
     """add() through the LDS-region partitioned pipeline (mode 1, forced) and the first-setter table
     (mode 0): per-key new flags, the count, the Redis bitmap bytes and length equal the oracle's
     in-order SETBIT fold, for a second batch that repeats keys within itself and re-adds keys of
-    the first batch."""
+    the first batch.  records: how the region kernel reports new keys -- 0 owner records,
+    1 non-owner records, 3 non-owner counters, 2 chosen from the sampled fill (the small filters
+    are more than half full for batch two)."""
     from redisson_amd import _lib as L_
 
     rng = np.random.default_rng(size % 997 + 31 * k + L)
@@ -770,6 +772,7 @@ def test_partitioned_add_parity(client, fresh, mode, size, k, L):
     f.tryInitRaw(size, k)
     ref = O.OracleBloom(size, k)
     assert L_.lib().rbx_tune(b"add_partition", mode) == 0
+    assert L_.lib().rbx_tune(b"add_records", records) == 0
     try:
         for a, o in arenas:
             cg, ng = f.addEach(a)
@@ -777,6 +780,7 @@ def test_partitioned_add_parity(client, fresh, mode, size, k, L):
             assert cg == cr and np.array_equal(ng, nr)
     finally:
         L_.lib().rbx_tune(b"add_partition", 2)
+        L_.lib().rbx_tune(b"add_records", 2)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()
@@ -795,10 +799,12 @@ def test_partitioned_add_overflow_falls_back(client, fresh):
     f.tryInitRaw(1 << 30, 7)
     ref = O.OracleBloom(1 << 30, 7)
     assert L_.lib().rbx_tune(b"add_partition", 1) == 0
+    assert L_.lib().rbx_tune(b"add_records", 1) == 0
     try:
         cg, ng = f.addEach(Arena.fixed(batch))
     finally:
         L_.lib().rbx_tune(b"add_partition", 2)
+        L_.lib().rbx_tune(b"add_records", 2)
     cr, nr = ref.add(*O.fixed_arena(batch), per_key=True)
     assert cg == cr and np.array_equal(ng, nr)
     assert f.exportBitmap() == ref.redis_string()
@@ -911,8 +917,9 @@ def test_multi_filter_table_cache_follows_handles(client, fresh):
 
 
 def test_partitioned_contains_deterministic_at_c2_scale(client, fresh):
-    """100M keys at C2 geometry: every partitioned call counts exactly what the direct kernel
-    counts (a lost or stray region pair would shift the count by a few keys)."""
+    """100M keys at C2 geometry: every partitioned call answers exactly what the direct kernel
+    answers, key by key (a lost or stray region pair would flip a few keys' flags), and the
+    counts agree with the flags."""
     import torch
 
     from redisson_amd import _lib as L
@@ -928,18 +935,72 @@ def test_partitioned_contains_deterministic_at_c2_scale(client, fresh):
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
     h.add_dev(device_keys(keys.data_ptr(), n // 2, 32), cnt.data_ptr())
     dk = device_keys(keys.data_ptr(), n, 32)
+    ref = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
     try:
         L.lib().rbx_tune(b"contains_partition", 0)
-        h.contains_dev(dk, cnt.data_ptr() + 8)
+        h.contains_dev(dk, cnt.data_ptr() + 8, ref.data_ptr())
         L.lib().rbx_tune(b"contains_partition", 1)
         for i in range(4):
-            h.contains_dev(dk, cnt.data_ptr() + 16 + 8 * i)
+            out.fill_(7)
+            h.contains_dev(dk, cnt.data_ptr() + 16 + 8 * i, out.data_ptr())
+            torch.cuda.synchronize()
+            diff = int((out != ref).sum())
+            assert diff == 0, (i, diff, torch.nonzero(out != ref)[:8].flatten().tolist())
     finally:
         L.lib().rbx_tune(b"contains_partition", 2)
     torch.cuda.synchronize()
     c = cnt.tolist()
-    assert c[1] >= n // 2 and c[2:6] == [c[1]] * 4, c
+    assert bool(ref[: n // 2].all()) and c[1] == int(ref.sum(dtype=torch.int64))
+    assert c[2:6] == [c[1]] * 4, c
     h.close()
     f.delete()
-    del keys
+    del keys, ref, out
+    torch.cuda.empty_cache()
+
+
+def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
+    """50M keys into a 2^32-bit filter (C2 add geometry), then the same 50M again: the
+    first-setter table and the partitioned add with owner records, non-owner records and non-owner
+    counters return the same per-key new flags and counts and leave identical bitmaps."""
+    import torch
+
+    from redisson_amd import _lib as L
+    from redisson_amd import device_keys
+
+    n = 50_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(12)
+    keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+    keys[n - 1000:] = keys[:1000]  # repeats inside the batch
+    dk = device_keys(keys.data_ptr(), n, 32)
+    runs = [(0, 2), (1, 0), (1, 1), (1, 3)]
+    flags, counts, bitmaps = [], [], []
+    try:
+        for i, (part, rec) in enumerate(runs):
+            nm = f"{fresh}-{i}"
+            f = client.getBloomFilter(nm)
+            f.tryInitRaw(1 << 32, 7)
+            h = BloomHandle(client, nm)
+            cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+            out = torch.zeros((2, n), dtype=torch.uint8, device="cuda")
+            L.lib().rbx_tune(b"add_partition", part)
+            L.lib().rbx_tune(b"add_records", rec)
+            for j in range(2):  # second pass: every key already present
+                h.add_dev(dk, cnt.data_ptr() + 8 * j, out[j].data_ptr())
+            torch.cuda.synchronize()
+            flags.append(out)
+            counts.append(cnt.tolist())
+            bitmaps.append(f.exportBitmap())
+            h.close()
+            f.delete()
+    finally:
+        L.lib().rbx_tune(b"add_partition", 2)
+        L.lib().rbx_tune(b"add_records", 2)
+    assert counts[0][1] == 0 and n - 1000 - 10 <= counts[0][0] <= n - 1000, counts[0]
+    for i in range(1, len(runs)):
+        assert counts[i] == counts[0], (runs[i], counts[i], counts[0])
+        assert torch.equal(flags[i], flags[0]), runs[i]
+        assert bitmaps[i] == bitmaps[0], runs[i]
+    del keys, flags
     torch.cuda.empty_cache()

@@ -39,6 +39,9 @@ def main():
     ap.add_argument("what", nargs="*", default=["gather", "stage1", "sizes", "add"])
     ap.add_argument("--keys", type=int, default=100_000_000)
     a = ap.parse_args()
+    for kv in filter(None, os.environ.get("RBX_TUNE", "").split(",")):  # process-wide rbx_tune settings
+        key, val = kv.split("=")
+        assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
@@ -226,6 +229,37 @@ def main():
         L.lib().rbx_tune(b"add_partition_diag", 0)
         for dg, v in res.items():
             print(json.dumps({"bench": "add_partition_diag", "diag": dg, "ms_median": statistics.median(v)}), flush=True)
+
+    if "addab" in a.what:
+        # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
+        # round, fresh filter per run: RBX_ADDAB="key=v,key=v;key=v" ("-" = defaults)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        variants = os.environ.get("RBX_ADDAB", "-;add_records=0").split(";")
+        res = {v: [] for v in variants}
+        news = {}
+        for rnd in range(5):
+            for v in variants:
+                for kv in filter(None, ("" if v == "-" else v).split(",")):
+                    key, val = kv.split("=")
+                    assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
+                fb = client.getBloomFilter(f"ab-{rnd}")
+                fb.tryInitRaw(1 << 32, 7)
+                h = BloomHandle(client, f"ab-{rnd}")
+                cnt.zero_()
+                res[v].append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(),
+                                                              stream=sp), 1))
+                news[v] = int(cnt[0].item())
+                h.close()
+                fb.delete()
+                for kv in filter(None, ("" if v == "-" else v).split(",")):
+                    key = kv.split("=")[0]
+                    L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2}.get(key, 0))
+        assert len(set(news.values())) == 1, news
+        for v, t in res.items():
+            med = statistics.median(t)
+            print(json.dumps({"bench": "addab", "tune": v, "keys": m, "ms_median": med, "ms_min": min(t),
+                              "ms_max": max(t), "keys_per_s": m / (med / 1e3), "new": news[v]}), flush=True)
 
     if "padd" in a.what:
         # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
