@@ -178,7 +178,7 @@ struct rbx_ctx {
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
-    DevBuf pa_p1, pa_p2, pa_cnt, pa_recs, pa_bits, pa_ctr;  // partitioned add
+    DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr;  // partitioned add
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     DevBuf hll_pack;                                // contiguous registers for the RCCL merge
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
@@ -498,7 +498,7 @@ static int g_add_partition_diag = 0;
 static int g_add_record_policy = 2;
 
 static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
-    if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << kBaRegionBits)) return false;
+    if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << 15)) return false;
     if (g_add_partition_mode == 0) return false;
     if (g_add_partition_mode == 1) return true;
     return size >= (1ULL << 26) && n >= (1ULL << 20);
@@ -519,11 +519,11 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     const uint32_t nregions = (uint32_t)((size + (1ULL << kBaRegionBits) - 1) >> kBaRegionBits);
     uint32_t L = 0;
     while ((1ULL << L) < nregions) ++L;
-    const uint32_t f3 = std::min<uint32_t>(6, L), f2 = std::min<uint32_t>(6, L - f3);
-    const uint32_t s3 = kBaRegionBits, s2 = s3 + f3, s1 = s2 + f2;
-    const uint32_t ncoarse = (uint32_t)((size + (1ULL << s1) - 1) >> s1);  // <= 64 for size <= 2^32
-    const uint32_t n2 = (uint32_t)((size + (1ULL << s2) - 1) >> s2);
-    // chunk: key ids < 2^26 and the per-region pair capacity fits the LDS record image
+    // two radix passes: stage 1 into 2^(L - f3) <= 256 buckets, one rebucket of fan-out 2^f3 <= 256
+    const uint32_t f3 = std::min<uint32_t>(8, L);
+    const uint32_t s3 = kBaRegionBits, s1 = s3 + f3;
+    const uint32_t ncoarse = (uint32_t)((size + (1ULL << s1) - 1) >> s1);  // <= 256 for size <= 2^32
+    // chunk: key ids < 2^26 and the expected pairs per region (x 1.3 slack) within the block's registers
     const double per_region = (double)k * (double)(1ULL << kBaRegionBits) / (double)size;  // pairs per key
     uint64_t chunk = (uint64_t)((kBaMaxRegionPairs - 512) / 1.3 / per_region);
     chunk = std::min<uint64_t>(chunk, 1ULL << 26);
@@ -536,22 +536,17 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         return (cap + round - 1) / round * round;
     };
     const uint64_t cap1 = cap_of(s1, 1.15 / kBkSub, 8192, 8192);
-    const uint64_t cap2 = cap_of(s2, 1.15, 8192, 8192);
     const uint64_t cap3 = std::min<uint64_t>(kBaMaxRegionPairs, cap_of(s3, 1.3, 256, 64));
-    const uint32_t nranges = (uint32_t)((chunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
-    const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;  // records per key range <= 2^20 keys x k
-    const uint64_t b1 = (uint64_t)ncoarse * kBkSub * cap1 * 8, b3 = (uint64_t)nregions * cap3 * 8;
-    RBX_TRY(c->pa_p1.reserve(std::max(b1, b3)));  // level 3 reuses level 1's buffer (consumed by level 2)
-    RBX_TRY(c->pa_p2.reserve((uint64_t)n2 * cap2 * 8));
-    const uint64_t ncnt = 64 * kBkSub + n2 + nregions + nranges + 2;
+    RBX_TRY(c->pa_p1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
+    RBX_TRY(c->pa_p2.reserve((uint64_t)nregions * cap3 * 8));
+    const uint64_t ncnt = (uint64_t)ncoarse * kBkSub + nregions + 2;
     RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
-    RBX_TRY(c->pa_recs.reserve((uint64_t)nranges * cap_rec * 4));
-    const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);
+    const uint64_t nbw = (chunk + 31) / 32;
     RBX_TRY(c->pa_bits.reserve(nbw * 4));
     // per-key non-owner counters (one byte per key; k_ba_keys zeroes what it read): zeroed once
     // when (re)allocated
-    if (c->pa_ctr.cap < ((uint64_t)nranges << kBaKeyRangeBits)) {
-        RBX_TRY(c->pa_ctr.reserve((uint64_t)nranges << kBaKeyRangeBits));
+    if (c->pa_ctr.cap < nbw * 32) {
+        RBX_TRY(c->pa_ctr.reserve(nbw * 32));
         HIP_TRY(hipMemsetAsync(c->pa_ctr.p, 0, c->pa_ctr.cap, st));
     }
     const int fl = fast_len(keys);
@@ -563,28 +558,18 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.f = f;
         a.ncoarse = ncoarse;
         a.s1 = s1;
-        a.s2 = s2;
         a.s3 = s3;
-        a.f2 = f2;
         a.f3 = f3;
-        a.n2 = n2;
         a.nregions = nregions;
         a.cap1 = cap1;
-        a.cap2 = cap2;
         a.cap3 = cap3;
-        a.cap_rec = cap_rec;
         a.p1 = c->pa_p1.as<unsigned long long>();
-        a.p2 = c->pa_p2.as<unsigned long long>();
-        a.p3 = a.p1;
+        a.p3 = c->pa_p2.as<unsigned long long>();
         a.cnt1 = c->pa_cnt.as<uint32_t>();
-        a.cnt2 = a.cnt1 + 64 * kBkSub;
-        a.cnt3 = a.cnt2 + n2;
-        a.rec_cnt = a.cnt3 + nregions;
-        a.overflow = a.rec_cnt + nranges;
+        a.cnt3 = a.cnt1 + (uint64_t)ncoarse * kBkSub;
+        a.overflow = a.cnt3 + nregions;
         a.mode = a.overflow + 1;
         a.record_policy = (uint32_t)g_add_record_policy;
-        a.recs = c->pa_recs.as<uint32_t>();
-        a.nranges = (uint32_t)((a.nchunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
         a.new_bits = c->pa_bits.as<uint32_t>();
         a.ctr = c->pa_ctr.as<uint32_t>();
         a.nwords4 = (size + 127) / 128 * 4;
@@ -592,7 +577,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.count = d_count;
         a.diag = (uint32_t)g_add_partition_diag;
         HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
-        HIP_TRY(hipMemsetAsync(a.new_bits, 0, ((uint64_t)a.nranges << (kBaKeyRangeBits - 5)) * 4, st));
+        HIP_TRY(hipMemsetAsync(a.new_bits, 0, (a.nchunk + 31) / 32 * 4, st));
         launch_add_partitioned_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
         uint32_t ovf = 0;
@@ -787,7 +772,7 @@ int rbx_shutdown(rbx_ctx *c) {
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
                           &c->counters, &c->filt_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
-                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_recs, &c->pa_bits, &c->pa_ctr, &c->st_adds,
+                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->st_adds,
                           &c->st_prefilter, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1]}) {
             if (b->p) (void)hipFree(b->p);
@@ -2622,11 +2607,10 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     // How the add's region kernel reports which keys are new (add_partitioned.hip k_ba_mode):
-    // 0 owner records, 1 non-owner records, 3 non-owner counters, 2 (default) chosen from the
-    // sampled fill (< 1/16: counters, < 1/2: non-owner records, else owner records).  Exact
-    // either way.
+    // 0 owner bits, 1 non-owner counters, 2 (default) counters while the sampled fill is below
+    // 1/2.  Exact either way.
     if (!strcmp(key, "add_records")) {
-        if (value < 0 || value > 3) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_records in [0, 3]");
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_records in [0, 2]");
         g_add_record_policy = value;
         return RBX_OK;
     }

@@ -89,31 +89,26 @@ void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream
 void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
-#ifndef RBX_BA_REGION_BITS
-#define RBX_BA_REGION_BITS 15
-#endif
-// 2^15-bit regions: owner array (128 KiB) + bitmap (4 KiB) in LDS (14: 64 KiB + 2 KiB, two blocks per CU)
-constexpr int kBaRegionBits = RBX_BA_REGION_BITS;
-constexpr int kBaKeyRangeBits = 20;             // records bucketed by 2^20-key ranges (128 KiB LDS bitmap)
-constexpr uint32_t kBaMaxRegionPairs = 6144u >> (15 - kBaRegionBits);  // LDS record image: cap3 <= this
+// Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB
+// of LDS, two blocks per CU); at most 8 pairs per thread of the 1024-thread region block.
+constexpr int kBaRegionBits = 16;
+constexpr uint32_t kBaMaxRegionPairs = 8192;  // cap3 <= this
 struct BaArgs {
     KeysDev keys;
     uint64_t base, nchunk;
     FilterDesc f;                 // bm, redis_len, mp, k
-    uint32_t ncoarse;             // level-1 buckets (each kBkSub sub-partitions)
-    uint32_t s1, s2, s3;          // partition id = idx >> s at levels 1, 2, 3 (s3 = kBaRegionBits)
-    uint32_t f2, f3;              // fan-out bits of levels 2 and 3
-    uint32_t n2, nregions;        // level-2 partitions, regions
-    uint64_t cap1, cap2, cap3, cap_rec;
-    unsigned long long *p1, *p2, *p3;  // pair arrays (p3 may alias p1)
-    uint32_t *cnt1, *cnt2, *cnt3, *rec_cnt;  // zeroed per chunk
-    uint32_t *recs;               // nranges x cap_rec owner key ids
-    uint32_t nranges;
-    uint32_t *new_bits;           // nranges x 2^15 words, zeroed per chunk
+    uint32_t ncoarse;             // level-1 buckets (<= 256, each kBkSub sub-partitions)
+    uint32_t s1, s3;              // level-1 bucket = idx >> s1, region = idx >> s3 (s3 = kBaRegionBits)
+    uint32_t f3;                  // fan-out bits of the rebucket (level 1 -> regions), <= 8
+    uint32_t nregions;
+    uint64_t cap1, cap3;
+    unsigned long long *p1, *p3;  // level-1 and region pair arrays
+    uint32_t *cnt1, *cnt3;        // zeroed per chunk
+    uint32_t *new_bits;           // ceil(nchunk / 32) words, zeroed per chunk
+    uint32_t *ctr;                // byte counter per key (nchunk rounded up to 32), all zero between calls
     uint32_t *overflow;           // zeroed; set when a pair does not fit (the chunk then reruns on the table path)
-    uint32_t *mode;               // written by k_ba_mode: 0 owner records, 1 non-owner records, 2 non-owner counters
-    uint32_t record_policy;       // rbx_tune "add_records": 0, 1, 3 = force mode 0, 1, 2; 2 = from the sampled fill
-    uint32_t *ctr;                // nranges x 2^20 byte counters (mode 2), all zero between calls
+    uint32_t *mode;               // written by k_ba_mode: 1 = non-owner counters, 0 = owner bits
+    uint32_t record_policy;       // rbx_tune "add_records": 0 owner bits, 1 counters, 2 from the sampled fill
     uint64_t nwords4;             // bitmap words rounded up to a multiple of 4
     uint8_t *out_new;
     unsigned long long *count;
