@@ -261,6 +261,42 @@ def main():
             print(json.dumps({"bench": "addab", "tune": v, "keys": m, "ms_median": med, "ms_min": min(t),
                               "ms_max": max(t), "keys_per_s": m / (med / 1e3), "new": news[v]}), flush=True)
 
+    if "addfill" in a.what:
+        # C2-size add (n/2 keys) into a 2^32-bit filter whose bitmap was imported with fill f
+        # (random bits: AND/OR of uniform bytes), each add_records mode, fresh import per run
+        import ctypes as C
+
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        nbytes = 1 << 29
+
+        def bits(f):
+            r = lambda: torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+            return {0.0: lambda: torch.zeros(nbytes, dtype=torch.uint8, device="cuda"), 0.125: lambda: r() & r() & r(),
+                    0.25: lambda: r() & r(), 0.5: r, 0.75: lambda: r() | r()}[f]()
+
+        for fill in (0.0, 0.125, 0.25, 0.5, 0.75):
+            img = bits(fill)
+            for rec in (0, 1, 2):
+                L.lib().rbx_tune(b"add_records", rec)
+                ts, news = [], None
+                for rnd in range(2):
+                    nm = f"af-{fill}-{rec}-{rnd}"
+                    fb = client.getBloomFilter(nm)
+                    fb.tryInitRaw(1 << 32, 7)
+                    assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), img.data_ptr(), nbytes, sp) == 0
+                    h = BloomHandle(client, nm)
+                    cnt.zero_()
+                    ts.append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(),
+                                                              stream=sp), 1))
+                    news = int(cnt[0].item())
+                    h.close()
+                    fb.delete()
+                print(json.dumps({"bench": "addfill", "fill": fill, "add_records": rec, "ms": min(ts), "new": news}),
+                      flush=True)
+            del img
+        L.lib().rbx_tune(b"add_records", 2)
+
     if "padd" in a.what:
         # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
