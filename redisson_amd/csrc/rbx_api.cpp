@@ -491,8 +491,11 @@ static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_fi
 }
 
 // Partitioned add (add_partitioned.hip) for one large filter.  Mode: 0 never, 1 whenever
-// k <= 16, 2 (default) when the bitmap is >= 8 MiB and the batch >= 1M keys (measured faster than
-// the first-setter table at every size from 8 MiB to 512 MiB: tools/microbench.py psizes).
+// k <= 16, 2 (default) when the bitmap is >= 8 MiB and the batch has >= max(2^17, size / 2^12)
+// keys.  The region pass reads and writes every touched region of the bitmap, so its floor
+// grows with the bitmap (0.7 ms at 512 MiB) while the table path's cost grows with the batch
+// (0.7 us per 1K keys): crossovers ~150K keys at 12-32 MiB, ~1M at 512 MiB
+// (tools/microbench.py addsweep, profiles/r02/r02h_addsweep_table_vs_partitioned.jsonl).
 static int g_add_partition_mode = 2;
 static int g_add_partition_diag = 0;
 static int g_add_record_policy = 2;
@@ -501,7 +504,7 @@ static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << 15)) return false;
     if (g_add_partition_mode == 0) return false;
     if (g_add_partition_mode == 1) return true;
-    return size >= (1ULL << 26) && n >= (1ULL << 20);
+    return size >= (1ULL << 26) && n >= std::max<uint64_t>(1ULL << 17, size >> 12);
 }
 
 static KeysDev keys_slice(const KeysDev &k, uint64_t i0, uint64_t n) {

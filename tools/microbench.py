@@ -297,6 +297,36 @@ def main():
             del img
         L.lib().rbx_tune(b"add_records", 2)
 
+    if "addsweep" in a.what:
+        # table vs partitioned add by batch size and filter size (fresh filter per run, 16-B keys)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        k16 = torch.randint(0, 256, (4_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+        for size in (1 << 24, 95_850_583, 1 << 28, 1 << 32):
+            for nk in (20_000, 100_000, 250_000, 500_000, 1_000_000, 4_000_000):
+                res = {}
+                for mode in (0, 1):
+                    L.lib().rbx_tune(b"add_partition", mode)
+                    ts = []
+                    for rnd in range(3):
+                        nm = f"as-{size}-{nk}-{mode}-{rnd}"
+                        fb = client.getBloomFilter(nm)
+                        fb.tryInitRaw(size, 7)
+                        h = BloomHandle(client, nm)
+                        h.add_dev(device_keys(k16.data_ptr(), nk, 16), cnt.data_ptr(), stream=sp)  # first call: allocations
+                        h.close()
+                        fb.delete()
+                        fb = client.getBloomFilter(nm)
+                        fb.tryInitRaw(size, 7)
+                        h = BloomHandle(client, nm)
+                        ts.append(timed(stream, lambda: h.add_dev(device_keys(k16.data_ptr(), nk, 16), cnt.data_ptr(),
+                                                                  stream=sp), 1))
+                        h.close()
+                        fb.delete()
+                    res[mode] = statistics.median(ts)
+                print(json.dumps({"bench": "addsweep", "size": size, "keys": nk, "table_ms": res[0],
+                                  "partitioned_ms": res[1]}), flush=True)
+        L.lib().rbx_tune(b"add_partition", 2)
+
     if "padd" in a.what:
         # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
