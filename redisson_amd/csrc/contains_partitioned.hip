@@ -356,11 +356,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const uint64_t w0 = (uint64_t)r * kBkRegionWords;
         const uint32_t nv = (uint32_t)min<uint64_t>(kBkRegionWords, nwords4 - w0) / 4;
         const u32x4 *srcv = (const u32x4 *)(bm + w0);
-        u32x4 b[kBkRegionWords / 4 / NT];
+        // the region's bitmap goes straight to LDS (global_load_lds, 16 B per lane, lane-linear):
+        // no VGPRs held for it, which also removed the kernel's register spills
 #pragma unroll
         for (uint32_t i = 0; i < kBkRegionWords / 4 / NT; ++i) {
             const uint32_t j = i * NT + threadIdx.x;
-            if (j < nv) b[i] = srcv[j];
+            if (j < nv)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(srcv + j),
+                                                 (__attribute__((address_space(3))) void *)((u32x4 *)s_bm + i * NT + wave * 64),
+                                                 16, 0, 0);
         }
         // cap2 is a multiple of 64 pairs: the region's lo words are 16-byte and hi halves 8-byte aligned
         const u32x4 *slo = (const u32x4 *)(p2lo + (uint64_t)r * cap2);
@@ -376,12 +380,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                 vh[u] = __builtin_nontemporal_load(shi + q);
             }
         }
-#pragma unroll
-        for (uint32_t i = 0; i < kBkRegionWords / 4 / NT; ++i) {
-            const uint32_t j = i * NT + threadIdx.x;
-            if (j < nv) ((u32x4 *)s_bm)[j] = b[i];
-        }
-        __syncthreads();
+        __syncthreads();  // waits for the bitmap DMA (and the first pair loads)
         for (uint32_t base = 0;;) {
 #pragma unroll
             for (uint32_t u = 0; u < G; ++u) {

@@ -327,6 +327,23 @@ def main():
                                   "partitioned_ms": res[1]}), flush=True)
         L.lib().rbx_tune(b"add_partition", 2)
 
+    if "c1add" in a.what:
+        # the C1 leg's add: 1M 16-byte keys into a fresh tryInit(1e7, 0.01) filter, 5 times
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        k16 = torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+        ts = []
+        for rnd in range(6):
+            nm = f"c1a-{rnd}"
+            fb = client.getBloomFilter(nm)
+            fb.tryInitRaw(95_850_583, 7)
+            h = BloomHandle(client, nm)
+            torch.cuda.synchronize()
+            ts.append(timed(stream, lambda: h.add_dev(device_keys(k16.data_ptr(), 1_000_000, 16), cnt.data_ptr(),
+                                                      stream=sp), 1))
+            h.close()
+            fb.delete()
+        print(json.dumps({"bench": "c1add", "ms": ts[1:], "median": statistics.median(ts[1:])}), flush=True)
+
     if "padd" in a.what:
         # add of n/2 keys into an empty filter: first-setter table (0) vs partitioned (1), fresh filters
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
