@@ -12,13 +12,18 @@
 //   B  k_ba_rebucket: level 1 -> regions (idx >> 16), fan-out <= 256
 //   C  k_ba_region  : region bitmap + met-once / met-again bitsets + a collision table in LDS;
 //                     owners set their bits; the bitmap is written back
-//   D  k_ba_keys    : non-owner counters -> new_bits
+//   D  k_ba_keys    : non-owner counters -> new_bits;  D' k_ba_keys_rec: owner records -> new_bits
 //   E  k_ba_final   : out_new bytes and the count
-// Reporting new keys: a key is new iff at least one of its k pairs owns its bit.  Into a mostly
-// empty filter nearly every pair owns, so C reports the rarer kind with one fire-and-forget
-// atomic per pair: below a sampled fill of 1/2 each non-owner pair bumps its key's byte counter
-// (the key is new iff its count < k; C2: only the ~4% in-batch collisions do), above it each
-// owner pair sets its key's bit in new_bits directly (k_ba_mode picks; rbx_tune "add_records").
+// Reporting new keys: a key is new iff at least one of its k pairs owns its bit.  k_ba_mode
+// samples the bitmap's fill per chunk and picks (rbx_tune "add_records" can force one):
+//   - below a fill of 3/32 each NON-OWNER pair bumps its key's byte counter with one
+//     fire-and-forget atomic (C2 into an empty filter: only the ~4% in-batch collisions do) and
+//     D turns counters into new bits (count < k);
+//   - otherwise the region kernel writes the OWNER pairs' key ids as runs bucketed by 2^20-key
+//     range (one reservation per range per region) and D' sets their bits in LDS images of the
+//     ranges' new_bits words -- streaming instead of one scattered atomic per report, so the
+//     add costs 5.0-5.9 ms for 50M keys at every fill (owner bits by direct atomics: 9.8 ms at
+//     fill 1/2, 15.8 ms at 0).
 // Chunks run strictly one after another (each chunk's regions are updated before the next
 // chunk's pairs are examined), so the in-order semantics hold across chunks.  Capacities are
 // sized for uniform bits; a batch that overflows one (adversarial repeats) sets `overflow`, the
@@ -206,8 +211,8 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
 }
 
 // mode -----------------------------------------------------------------------------------
-// Sampled fill of the bitmap -> how C reports new keys (see the header): 1 = non-owner counters
-// (fill below 1/2: non-owners are the rarer kind), 0 = owner bits.
+// Sampled fill of the bitmap -> how C reports new keys (see the header): 1 = non-owner counters,
+// 2 = owner records, 0 = owner bits.
 __global__ __launch_bounds__(1024) void k_ba_mode(const uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t policy,
                                                   uint32_t *__restrict__ mode) {
     __shared__ uint32_t s_sum[16];
@@ -225,11 +230,13 @@ __global__ __launch_bounds__(1024) void k_ba_mode(const uint32_t *__restrict__ b
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        uint32_t m = policy;
+        uint32_t m = policy == 3 ? 2u : policy;
         if (policy == 2) {
             uint32_t t = 0;
             for (int w = 0; w < 16; ++w) t += s_sum[w];
-            m = t < 4096u * 16u ? 1u : 0u;  // sampled fill below 1/2
+            // sampled fill f = t / (4096 * 32): non-owner counters below 3/32, owner records
+            // above (owner bits never measured faster: profiles/r02/r02j_addfill_modes.jsonl)
+            m = t < 4096u * 3u ? 1u : 2u;
         }
         *mode = m;
     }
@@ -256,6 +263,7 @@ __device__ __forceinline__ uint32_t ba_slot(uint32_t off, uint32_t t) {
 __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ba_region(
     const unsigned long long *__restrict__ p3, const uint32_t *__restrict__ cnt3, uint64_t cap3, uint32_t nregions,
     uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t *__restrict__ new_bits, uint32_t *__restrict__ ctr,
+    uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt, uint64_t cap_rec, uint32_t nranges,
     const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t diag) {
     constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, T = 1u << kBaTableBits;
     constexpr uint32_t kOff = (1u << kBaRegionBits) - 1;
@@ -264,9 +272,13 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     __shared__ __attribute__((aligned(16))) uint32_t s_seen[kBaRegionWords];   // met at 0 by a pair
     __shared__ __attribute__((aligned(16))) uint32_t s_multi[kBaRegionWords];  // met at 0 by >= 2 pairs
     __shared__ uint32_t s_toff[T], s_tmin[T];                                  // 8 KiB
+    __shared__ uint32_t s_rec[kBaMaxRegionPairs];                              // owner records, 32 KiB
+    __shared__ uint32_t s_rc[64], s_rst[64], s_rpos[64], s_rgb[64];
     static_assert(NV <= NT, "one u32x4 of the region per thread");
     if (*overflow) return;
-    const bool counters = *mode != 0;
+    const uint32_t md = *mode;
+    const bool counters = md == 1, records = md == 2, bits = md == 0;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long e[PER];
     bool loaded = false;
     for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
@@ -302,6 +314,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             s_toff[i] = ~0u;
             s_tmin[i] = ~0u;
         }
+        if (threadIdx.x < 64) s_rc[threadIdx.x] = 0;
         __syncthreads();
         // pass 1: which pairs meet a 0 bit, and which of those bits are met more than once
         uint32_t zm = 0;
@@ -368,14 +381,39 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             const uint32_t idx = (uint32_t)(e[p] >> 32), key = (uint32_t)e[p];
             if (own & (1u << p)) {
                 atomicOr(&s_bm[(idx & kOff) >> 5], bit_in_word(idx));
-                if (!counters && !(diag & 4)) atomicOr(&new_bits[key >> 5], 1u << (key & 31));
+                if (diag & 4) continue;
+                if (bits) atomicOr(&new_bits[key >> 5], 1u << (key & 31));
+                else if (records) atomicAdd(&s_rc[key >> kBaKeyRangeBits], 1u);
             } else if (counters && !(diag & 4) && p * NT + threadIdx.x < n) {
                 atomicAdd(&ctr[key >> 2], 1u << (8 * (key & 3)));  // no return: not waited on here
             }
         }
         if (!__syncthreads_or(own != 0u)) continue;  // uniform: no bit changed
         if (has_words) ((u32x4 *)(bm + w0))[threadIdx.x] = ((const u32x4 *)s_bm)[threadIdx.x];
-        __syncthreads();  // s_bm reuse
+        if (records && !(diag & 4)) {  // uniform: owner key ids as runs per 2^20-key range
+            uint32_t gb = 0;
+            const uint32_t q = threadIdx.x - 128;
+            const bool reserver = threadIdx.x >= 128 && q < nranges;
+            if (threadIdx.x < 64) bk_scan128(s_rc, nranges, s_rst, s_rpos);
+            else if (reserver && s_rc[q]) gb = atomicAdd(&rec_cnt[q], s_rc[q]);
+            __syncthreads();
+#pragma unroll
+            for (uint32_t p = 0; p < PER; ++p) {
+                if (own & (1u << p)) {
+                    const uint32_t key = (uint32_t)e[p];
+                    s_rec[atomicAdd(&s_rpos[key >> kBaKeyRangeBits], 1u)] = key;
+                }
+            }
+            if (reserver) s_rgb[q] = gb;
+            __syncthreads();
+            // records per range <= 2^20 keys x k = cap_rec: no overflow
+            for (uint32_t rq = wave; rq < nranges; rq += NT / 64) {
+                const uint32_t rn = s_rc[rq], st = s_rst[rq];
+                uint32_t *dst = recs + (uint64_t)rq * cap_rec + s_rgb[rq];
+                for (uint32_t t = lane; t < rn; t += 64) run_store(s_rec[st + t], dst + t);
+            }
+        }
+        __syncthreads();  // s_bm / s_rec reuse
     }
 }
 
@@ -385,7 +423,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
 __global__ __launch_bounds__(256) void k_ba_keys(uint32_t *__restrict__ ctr, uint64_t nchunk, uint32_t k,
                                                  uint32_t *__restrict__ new_bits, const uint32_t *__restrict__ overflow,
                                                  const uint32_t *__restrict__ mode) {
-    if (*overflow || *mode == 0) return;
+    if (*overflow || *mode != 1) return;
     const uint64_t nw = (nchunk + 31) >> 5;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
         u32x4 *src = (u32x4 *)(ctr + 8 * w);
@@ -399,6 +437,54 @@ __global__ __launch_bounds__(256) void k_ba_keys(uint32_t *__restrict__ ctr, uin
         new_bits[w] = v;
         if (a.x | a.y | a.z | a.w) src[0] = u32x4{0u, 0u, 0u, 0u};
         if (b.x | b.y | b.z | b.w) src[1] = u32x4{0u, 0u, 0u, 0u};
+    }
+}
+
+// Owner records -> new_bits: item = (key range q, slice s of 2^20 records): the slice's key ids
+// set bits of a 128 KiB LDS image of the range's new_bits words, whose nonzero words are OR-ed in.
+constexpr uint32_t kBaRangeWords = 1u << (kBaKeyRangeBits - 5);  // 32768
+
+__global__ __launch_bounds__(1024) void k_ba_keys_rec(const uint32_t *__restrict__ recs,
+                                                      const uint32_t *__restrict__ rec_cnt, uint64_t cap_rec,
+                                                      uint32_t nranges, uint32_t nslices,
+                                                      uint32_t *__restrict__ new_bits,
+                                                      const uint32_t *__restrict__ overflow,
+                                                      const uint32_t *__restrict__ mode) {
+    constexpr uint32_t NT = 1024;
+    __shared__ uint32_t s_bits[kBaRangeWords];  // 128 KiB
+    if (*overflow || *mode != 2) return;
+    const uint32_t nitems = nranges * nslices;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const uint32_t q = item % nranges, sl = item / nranges;
+        const uint64_t nrec = min<uint64_t>(rec_cnt[q], cap_rec);
+        const uint64_t start = (uint64_t)sl << kBaKeyRangeBits;
+        if (start >= nrec) continue;  // uniform
+        const uint32_t m = (uint32_t)min<uint64_t>(1ULL << kBaKeyRangeBits, nrec - start);
+        for (uint32_t w = threadIdx.x; w < kBaRangeWords; w += NT) s_bits[w] = 0u;
+        __syncthreads();
+        const uint32_t *src = recs + (uint64_t)q * cap_rec + start;
+        uint32_t i = threadIdx.x;
+        for (; i + 7 * NT < m; i += 8 * NT) {
+            uint32_t kk[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kk[u] = __builtin_nontemporal_load(src + i + u * NT);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t l = kk[u] & ((1u << kBaKeyRangeBits) - 1);
+                atomicOr(&s_bits[l >> 5], 1u << (l & 31));
+            }
+        }
+        for (; i < m; i += NT) {
+            const uint32_t l = src[i] & ((1u << kBaKeyRangeBits) - 1);
+            atomicOr(&s_bits[l >> 5], 1u << (l & 31));
+        }
+        __syncthreads();
+        uint32_t *dst = new_bits + (uint64_t)q * kBaRangeWords;
+        for (uint32_t w = threadIdx.x; w < kBaRangeWords; w += NT) {
+            const uint32_t v = s_bits[w];
+            if (v) atomicOr(&dst[w], v);
+        }
+        __syncthreads();
     }
 }
 
@@ -444,7 +530,10 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBkSub, it1, a.s3,
                        a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
     hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(kBaRegionThreads), 0, st, a.p3,
-                       a.cnt3, a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.overflow, a.mode, a.diag);
+                       a.cnt3, a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
+                       a.nranges, a.overflow, a.mode, a.diag);
+    hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
+                       a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
     hipLaunchKernelGGL(k_ba_keys, dim3(grid_for_pc((a.nchunk + 31) / 32)), dim3(256), 0, st, a.ctr, a.nchunk, a.f.k,
                        a.new_bits, a.overflow, a.mode);
     hipLaunchKernelGGL(k_ba_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.new_bits, a.nchunk, a.base,

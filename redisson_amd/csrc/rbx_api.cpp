@@ -178,7 +178,7 @@ struct rbx_ctx {
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
-    DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr;  // partitioned add
+    DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     DevBuf hll_pack;                                // contiguous registers for the RCCL merge
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
@@ -542,9 +542,12 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     const uint64_t cap3 = std::min<uint64_t>(kBaMaxRegionPairs, cap_of(s3, 1.3, 256, 64));
     RBX_TRY(c->pa_p1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
     RBX_TRY(c->pa_p2.reserve((uint64_t)nregions * cap3 * 8));
-    const uint64_t ncnt = (uint64_t)ncoarse * kBkSub + nregions + 2;
+    const uint32_t nranges = (uint32_t)((chunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
+    const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;  // a range's owner records <= 2^20 keys x k
+    RBX_TRY(c->pa_recs.reserve((uint64_t)nranges * cap_rec * 4));
+    const uint64_t ncnt = (uint64_t)ncoarse * kBkSub + nregions + nranges + 2;
     RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
-    const uint64_t nbw = (chunk + 31) / 32;
+    const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);  // whole ranges (the records kernel's images)
     RBX_TRY(c->pa_bits.reserve(nbw * 4));
     // per-key non-owner counters (one byte per key; k_ba_keys zeroes what it read): zeroed once
     // when (re)allocated
@@ -570,8 +573,12 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.p3 = c->pa_p2.as<unsigned long long>();
         a.cnt1 = c->pa_cnt.as<uint32_t>();
         a.cnt3 = a.cnt1 + (uint64_t)ncoarse * kBkSub;
-        a.overflow = a.cnt3 + nregions;
+        a.rec_cnt = a.cnt3 + nregions;
+        a.overflow = a.rec_cnt + nranges;
         a.mode = a.overflow + 1;
+        a.recs = c->pa_recs.as<uint32_t>();
+        a.cap_rec = cap_rec;
+        a.nranges = (uint32_t)((a.nchunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
         a.record_policy = (uint32_t)g_add_record_policy;
         a.new_bits = c->pa_bits.as<uint32_t>();
         a.ctr = c->pa_ctr.as<uint32_t>();
@@ -580,7 +587,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.count = d_count;
         a.diag = (uint32_t)g_add_partition_diag;
         HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
-        HIP_TRY(hipMemsetAsync(a.new_bits, 0, (a.nchunk + 31) / 32 * 4, st));
+        HIP_TRY(hipMemsetAsync(a.new_bits, 0, (uint64_t)a.nranges << (kBaKeyRangeBits - 5) << 2, st));
         launch_add_partitioned_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
         uint32_t ovf = 0;
@@ -775,7 +782,7 @@ int rbx_shutdown(rbx_ctx *c) {
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
                           &c->counters, &c->filt_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
-                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->st_adds,
+                          &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1]}) {
             if (b->p) (void)hipFree(b->p);
@@ -2610,10 +2617,10 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     // How the add's region kernel reports which keys are new (add_partitioned.hip k_ba_mode):
-    // 0 owner bits, 1 non-owner counters, 2 (default) counters while the sampled fill is below
-    // 1/2.  Exact either way.
+    // 0 owner bits, 1 non-owner counters, 3 owner records, 2 (default) chosen from the sampled
+    // fill.  Exact either way.
     if (!strcmp(key, "add_records")) {
-        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_records in [0, 2]");
+        if (value < 0 || value > 3) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_records in [0, 3]");
         g_add_record_policy = value;
         return RBX_OK;
     }

@@ -93,6 +93,7 @@ void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 // of LDS, two blocks per CU); at most 8 pairs per thread of the 1024-thread region block.
 constexpr int kBaRegionBits = 16;
 constexpr uint32_t kBaMaxRegionPairs = 8192;  // cap3 <= this
+constexpr int kBaKeyRangeBits = 20;           // owner records are bucketed by 2^20-key range
 struct BaArgs {
     KeysDev keys;
     uint64_t base, nchunk;
@@ -106,9 +107,12 @@ struct BaArgs {
     uint32_t *cnt1, *cnt3;        // zeroed per chunk
     uint32_t *new_bits;           // ceil(nchunk / 32) words, zeroed per chunk
     uint32_t *ctr;                // byte counter per key (nchunk rounded up to 32), all zero between calls
+    uint32_t *recs, *rec_cnt;     // owner records: nranges x cap_rec key ids, counts (zeroed per chunk)
+    uint64_t cap_rec;             // k x 2^20: a range's records never exceed it
+    uint32_t nranges;             // 2^20-key ranges of the chunk
     uint32_t *overflow;           // zeroed; set when a pair does not fit (the chunk then reruns on the table path)
-    uint32_t *mode;               // written by k_ba_mode: 1 = non-owner counters, 0 = owner bits
-    uint32_t record_policy;       // rbx_tune "add_records": 0 owner bits, 1 counters, 2 from the sampled fill
+    uint32_t *mode;               // written by k_ba_mode: 1 non-owner counters, 2 owner records, 0 owner bits
+    uint32_t record_policy;       // rbx_tune "add_records": 0 owner bits, 1 counters, 3 owner records, 2 from the sampled fill
     uint64_t nwords4;             // bitmap words rounded up to a multiple of 4
     uint8_t *out_new;
     unsigned long long *count;

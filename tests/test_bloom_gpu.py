@@ -744,7 +744,7 @@ def test_pinned_host_arena(client, fresh):
         L_.lib().rbx_host_free(p)
 
 
-@pytest.mark.parametrize("mode,records", [(0, 2), (1, 2), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mode,records", [(0, 2), (1, 2), (1, 0), (1, 1), (1, 3)])
 @pytest.mark.parametrize("size,k,L", [(1 << 32, 7, 32), (4294967293, 7, 32), (300_000_007, 10, 16),
                                       ((1 << 29) + 3, 16, 0), (1 << 20, 3, 24), (100_003, 2, 64)])
 def test_partitioned_add_parity(client, fresh, mode, records, size, k, L):
@@ -752,8 +752,8 @@ def test_partitioned_add_parity(client, fresh, mode, records, size, k, L):
     (mode 0): per-key new flags, the count, the Redis bitmap bytes and length equal the oracle's
     in-order SETBIT fold, for a second batch that repeats keys within itself and re-adds keys of
     the first batch.  records: how the region kernel reports new keys -- 0 owner bits,
-    1 non-owner counters, 2 chosen from the sampled fill (the small filters are more than half
-    full for batch two)."""
+    1 non-owner counters, 3 owner records, 2 chosen from the sampled fill (the small filters are
+    more than half full for batch two)."""
     from redisson_amd import _lib as L_
 
     rng = np.random.default_rng(size % 997 + 31 * k + L)
@@ -786,7 +786,7 @@ def test_partitioned_add_parity(client, fresh, mode, records, size, k, L):
     f.delete()
 
 
-@pytest.mark.parametrize("records", [0, 1])
+@pytest.mark.parametrize("records", [0, 1, 3])
 def test_partitioned_add_collision_table_rounds(client, fresh, records):
     """Every key twice in one 2^16-bit region: ~3000 bits are met by two pairs, three times the
     region kernel's 1024-slot collision table, so the table is cleared and refilled for further
@@ -990,8 +990,8 @@ def test_partitioned_contains_deterministic_at_c2_scale(client, fresh):
 
 def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     """50M keys into a 2^32-bit filter (C2 add geometry), then the same 50M again: the
-    first-setter table and the partitioned add reporting owner bits and non-owner counters return
-    the same per-key new flags and counts and leave identical bitmaps."""
+    first-setter table and the partitioned add reporting owner bits, non-owner counters and owner
+    records return the same per-key new flags and counts and leave identical bitmaps."""
     import torch
 
     from redisson_amd import _lib as L
@@ -1003,7 +1003,7 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
     keys[n - 1000:] = keys[:1000]  # repeats inside the batch
     dk = device_keys(keys.data_ptr(), n, 32)
-    runs = [(0, 2), (1, 0), (1, 1)]
+    runs = [(0, 2), (1, 0), (1, 1), (1, 3)]
     flags, counts, bitmaps = [], [], []
     try:
         for i, (part, rec) in enumerate(runs):

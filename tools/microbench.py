@@ -277,7 +277,7 @@ def main():
 
         for fill in (0.0, 0.125, 0.25, 0.5, 0.75):
             img = bits(fill)
-            for rec in (0, 1, 2):
+            for rec in [int(x) for x in os.environ.get("RBX_ADDFILL_MODES", "0,1,2").split(",")]:
                 L.lib().rbx_tune(b"add_records", rec)
                 ts, news = [], None
                 for rnd in range(2):
