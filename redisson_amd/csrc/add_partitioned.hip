@@ -534,7 +534,9 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
                        a.nranges, a.overflow, a.mode, a.diag);
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
-    hipLaunchKernelGGL(k_ba_keys, dim3(grid_for_pc((a.nchunk + 31) / 32)), dim3(256), 0, st, a.ctr, a.nchunk, a.f.k,
+    // one thread per new_bits word (32 keys): the per-thread chain of a smaller grid was the C1 add's third-largest cost
+    hipLaunchKernelGGL(k_ba_keys, dim3((unsigned)std::min<uint64_t>(2048, ((a.nchunk + 31) / 32 + 255) / 256)), dim3(256),
+                       0, st, a.ctr, a.nchunk, a.f.k,
                        a.new_bits, a.overflow, a.mode);
     hipLaunchKernelGGL(k_ba_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.new_bits, a.nchunk, a.base,
                        a.out_new, a.count, a.overflow);
