@@ -327,6 +327,26 @@ def main():
                                   "partitioned_ms": res[1]}), flush=True)
         L.lib().rbx_tune(b"add_partition", 2)
 
+    if "c1con" in a.what:
+        # the C1 leg's contains: 1M added + 1M fresh 16-byte keys against tryInit(1e7, 0.01)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        k16 = torch.randint(0, 256, (2_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+        fb = client.getBloomFilter("c1c")
+        fb.tryInitRaw(95_850_583, 7)
+        h = BloomHandle(client, "c1c")
+        h.add_dev(device_keys(k16.data_ptr(), 1_000_000, 16), cnt.data_ptr(), stream=sp)
+        torch.cuda.synchronize()
+        res = {}
+        for s1 in [int(x) for x in os.environ.get("RBX_C1_STAGE1", "4").split(",")]:
+            L.lib().rbx_tune(b"contains_stage1", s1)
+            ts = [timed(stream, lambda: h.contains_dev(device_keys(k16.data_ptr(), 2_000_000, 16), cnt.data_ptr() + 8,
+                                                       stream=sp), 5) for _ in range(5)]
+            res[s1] = statistics.median(ts)
+        L.lib().rbx_tune(b"contains_stage1", 4)
+        print(json.dumps({"bench": "c1con", "ms_by_stage1": res}), flush=True)
+        h.close()
+        fb.delete()
+
     if "c1add" in a.what:
         # the C1 leg's add: 1M 16-byte keys into a fresh tryInit(1e7, 0.01) filter, 5 times
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
