@@ -53,6 +53,31 @@ __device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uin
     if (2 * lane + 1 < nb) start[2 * lane + 1] = pos[2 * lane + 1] = ex + a;
 }
 
+// exclusive scan of cnt[j] + car[j] (j < nb <= 128) by wave 0: start[j] = the bucket's image
+// offset (its carried entries first), pos[j] = start[j] + car[j] (where its new entries go)
+__device__ __forceinline__ void bk_scan128c(const uint32_t *cnt, const uint32_t *car, uint32_t nb, uint32_t *start,
+                                            uint32_t *pos) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ca = 2 * lane < nb ? car[2 * lane] : 0u, cb = 2 * lane + 1 < nb ? car[2 * lane + 1] : 0u;
+    const uint32_t a = (2 * lane < nb ? cnt[2 * lane] : 0u) + ca;
+    const uint32_t b = (2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u) + cb;
+    uint32_t x = a + b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    const uint32_t ex = x - a - b;
+    if (2 * lane < nb) {
+        start[2 * lane] = ex;
+        pos[2 * lane] = ex + ca;
+    }
+    if (2 * lane + 1 < nb) {
+        start[2 * lane + 1] = ex + a;
+        pos[2 * lane + 1] = ex + a + cb;
+    }
+}
+
 // the same for nb <= 256 (four buckets per lane)
 __device__ __forceinline__ void bk_scan256(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
     const uint32_t lane = threadIdx.x;

@@ -85,12 +85,16 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
                                                    unsigned long long *__restrict__ miss, uint32_t flags) {
     constexpr int PER = bk_per<KMAX>();
     constexpr int TILE = NT * PER;
+    // dynamic LDS (bk_stage1_lds): image of a tile's pairs with each bucket's carried pairs in
+    // front of its new ones, the bucket id of every image slot, the carries, the counters
     extern __shared__ __attribute__((aligned(16))) unsigned char bk_lds[];
-    unsigned long long *s_img = (unsigned long long *)bk_lds;  // [TILE * (KMAX-1)]
-    unsigned long long *s_car = s_img + TILE * (KMAX - 1);      // [128 * kBkLine1] carried pairs
-    uint32_t *s_cnt = (uint32_t *)(s_car + 128 * kBkLine1);      // [128]
+    const uint32_t nimg = TILE * (k - 1) + 128 * (kBkLine1 - 1);
+    unsigned long long *s_img = (unsigned long long *)bk_lds;   // [nimg]
+    unsigned long long *s_car = s_img + nimg;                     // [128 * kBkLine1] carried pairs
+    uint32_t *s_cnt = (uint32_t *)(s_car + 128 * kBkLine1);       // [128]
     uint32_t *s_start = s_cnt + 128, *s_pos = s_start + 128, *s_gb = s_pos + 128, *s_full = s_gb + 128,
-             *s_cn = s_full + 128;
+             *s_cn = s_full + 128, *s_ncn = s_cn + 128;
+    uint8_t *s_bkt = (uint8_t *)(s_ncn + 128);                    // [nimg]
     const uint64_t ntiles = (nchunk + TILE - 1) / TILE;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t sub = blockIdx.x % kBkSub;
@@ -139,14 +143,24 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
             }
         }
         __syncthreads();
-        if (threadIdx.x < 64) bk_scan128(s_cnt, ncoarse, s_start, s_pos);
+        if (threadIdx.x < 64) bk_scan128c(s_cnt, s_cn, ncoarse, s_start, s_pos);
         else if (threadIdx.x >= 128 && threadIdx.x - 128 < ncoarse) {
             const uint32_t b = threadIdx.x - 128;
-            const uint32_t full = (s_cn[b] + s_cnt[b]) & ~(kBkLine1 - 1);
+            const uint32_t tot = s_cn[b] + s_cnt[b];
+            const uint32_t full = tot & ~(kBkLine1 - 1);
             s_full[b] = full;
+            s_ncn[b] = tot - full;
             s_gb[b] = full ? atomicAdd(&cnt1[b * kBkSub + sub], full) : 0u;
         }
         __syncthreads();
+        // the carried pairs go in front of their bucket's new ones
+        for (uint32_t j = threadIdx.x; j < ncoarse * kBkLine1; j += NT) {
+            const uint32_t b = j / kBkLine1, t = j % kBkLine1;
+            if (t < s_cn[b]) {
+                s_img[s_start[b] + t] = s_car[j];
+                s_bkt[s_start[b] + t] = (uint8_t)b;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             if (surv[q] && !(flags & 4)) {
@@ -154,28 +168,30 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
 #pragma unroll
                 for (int j = 1; j < KMAX; ++j) {
                     if ((uint32_t)j < k) {
-                        const uint32_t slot = atomicAdd(&s_pos[idx[q][j - 1] >> cshift], 1u);
+                        const uint32_t b = idx[q][j - 1] >> cshift;
+                        const uint32_t slot = atomicAdd(&s_pos[b], 1u);
                         s_img[slot] = ((unsigned long long)idx[q][j - 1] << 32) | key;
+                        s_bkt[slot] = (uint8_t)b;
                     }
                 }
             }
         }
         __syncthreads();
-        for (uint32_t b = wave; b < ncoarse; b += NT / 64) {
-            const uint32_t n = s_cnt[b], cn = s_cn[b], full = s_full[b], st = s_start[b];
-            unsigned long long *dst = pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + s_gb[b];
-            const uint64_t room = cap1 - min<uint64_t>(cap1, s_gb[b]);
-            for (uint32_t t = lane; t < full; t += 64) {  // carried pairs first, then this tile's run
-                const unsigned long long e = t < cn ? s_car[b * kBkLine1 + t] : s_img[st + t - cn];
-                if (t < room) run_store(e, dst + t);
+        // slot-linear: each bucket's first `full` entries (whole lines) go to its reservation, the
+        // rest become its carry; all lanes store, consecutive lanes to consecutive addresses
+        const uint32_t total = s_start[ncoarse - 1] + s_full[ncoarse - 1] + s_ncn[ncoarse - 1];
+        if (threadIdx.x < ncoarse) s_cn[threadIdx.x] = s_ncn[threadIdx.x];  // carries were placed above
+        for (uint32_t i = threadIdx.x; i < total; i += NT) {
+            const uint32_t b = s_bkt[i];
+            const uint32_t pos = i - s_start[b];
+            const unsigned long long e = s_img[i];
+            if (pos < s_full[b]) {
+                const uint64_t gp = (uint64_t)s_gb[b] + pos;
+                if (gp < cap1) run_store(e, pairs1 + (uint64_t)(b * kBkSub + sub) * cap1 + gp);
                 else bk_direct(e, bm, miss);
+            } else {
+                s_car[b * kBkLine1 + pos - s_full[b]] = e;
             }
-            if (full == 0) {  // cn + n < one line: append the run to the carry
-                for (uint32_t t = lane; t < n; t += 64) s_car[b * kBkLine1 + cn + t] = s_img[st + t];
-            } else {          // the remainder is the run's tail (full > cn)
-                for (uint32_t t = lane; t < cn + n - full; t += 64) s_car[b * kBkLine1 + t] = s_img[st + full - cn + t];
-            }
-            if (lane == 0) s_cn[b] = cn + n - full;
         }
         __syncthreads();  // LDS reuse
     }
@@ -512,7 +528,8 @@ static void bk_stage1(const PcArgs &a, hipStream_t st) {
     constexpr int TILE = NT1 * bk_per<KMAX>();
     const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
     const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 4096);
-    const size_t lds1 = (size_t)TILE * (KMAX - 1) * 8 + 128 * kBkLine1 * 8 + 6 * 128 * 4;
+    const size_t nimg = (size_t)TILE * (a.k - 1) + 128 * (kBkLine1 - 1);
+    const size_t lds1 = nimg * 8 + 128 * kBkLine1 * 8 + 7 * 128 * 4 + nimg;
     hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX, NT1>), dim3(g1), dim3(NT1), lds1, st, a.keys, a.base, a.nchunk, a.bm,
                        a.mp, a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
 }
