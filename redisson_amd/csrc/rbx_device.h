@@ -113,12 +113,6 @@ RBX_HD void hh_reset(HH &s) {
     s.v1[2] = kMul1[2] ^ swap32c(kKey2); s.v1[3] = kMul1[3] ^ swap32c(kKey3);
 }
 
-// zipperMerge0/1 (HighwayHash.java:248-260) on 32-bit halves.  With a = lower-lane
-// operand (Java's "v0" parameter) and b = upper (Java's "v1"), byte j of the result:
-//   zm0 = [a3 b4 a2 a5 | b6 a1 b7 a0]      zm1 = [b3 a4 b2 b5 | b1 a6 b0 a7]
-// Each half is 1-2 v_perm_b32 byte shuffles after selection by the compiler.
-RBX_HD uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xffu; }
-
 // v_perm_b32: byte i of the result = byte sel[i] of the 8-byte value {hi:x, lo:y}
 // (selectors 0-3 pick y, 4-7 pick x, 0x0c gives 0).  The host build emulates it so the
 // CPU self-test exercises the same byte plans.
@@ -137,6 +131,32 @@ RBX_HD uint32_t perm_b32(uint32_t x, uint32_t y, uint32_t sel) {
 #endif
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Two 32-bit halves as one 64-bit value.  On the device this is a bit cast (a register
+// pair): written as `hi << 32 | lo` the compiler turned `x += w2(lo, hi)` into two 64-bit
+// adds plus register copies (tools/hashbench.hip: 645 -> 495 VALU instructions per hash).
+RBX_HD uint64_t w2(uint32_t lo, uint32_t hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bit_cast(uint64_t, u32x2{lo, hi});
+#else
+    return ((uint64_t)hi << 32) | lo;
+#endif
+}
+
+// 64-bit add of an operand given as halves, as an add-with-carry pair (finalize's swapped
+// operands: no register copies to form a pair)
+RBX_HD uint64_t add_halves(uint64_t x, uint32_t lo, uint32_t hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned int c;
+    const uint32_t l = __builtin_addc((uint32_t)x, lo, 0u, &c);
+    return w2(l, (uint32_t)(x >> 32) + hi + c);
+#else
+    return x + w2(lo, hi);
+#endif
+}
+
 // zipperMerge0/1 (HighwayHash.java:248-260).  With a = lower-lane operand (Java's "v0"
 // parameter) and b = upper (Java's "v1"), byte j of the result:
 //   zm0 = [a3 b4 a2 a5 | b6 a1 b7 a0]      zm1 = [b3 a4 b2 b5 | b1 a6 b0 a7]
@@ -144,30 +164,22 @@ RBX_HD uint32_t perm_b32(uint32_t x, uint32_t y, uint32_t sel) {
 // word two (one perm).
 RBX_HD uint64_t zipper0(uint64_t b, uint64_t a) {
     const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bh = (uint32_t)(b >> 32);
-    const uint32_t t = perm_b32(bh, al, 0x0C020403u);   // [a3 b4 a2 0]
-    const uint32_t lo = perm_b32(ah, t, 0x05020100u);   // [a3 b4 a2 a5]
-    const uint32_t hi = perm_b32(bh, al, 0x00070106u);  // [b6 a1 b7 a0]
-    return ((uint64_t)hi << 32) | lo;
+    const uint32_t t = perm_b32(bh, al, 0x0C020403u);                           // [a3 b4 a2 0]
+    return w2(perm_b32(ah, t, 0x05020100u), perm_b32(bh, al, 0x00070106u));  // [a3 b4 a2 a5 | b6 a1 b7 a0]
 }
 
 RBX_HD uint64_t zipper1(uint64_t b, uint64_t a) {
     const uint32_t ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
-    const uint32_t t = perm_b32(ah, bl, 0x0C020403u);   // [b3 a4 b2 0]
-    const uint32_t lo = perm_b32(bh, t, 0x05020100u);   // [b3 a4 b2 b5]
-    const uint32_t hi = perm_b32(ah, bl, 0x07000601u);  // [b1 a6 b0 a7]
-    return ((uint64_t)hi << 32) | lo;
+    const uint32_t t = perm_b32(ah, bl, 0x0C020403u);                           // [b3 a4 b2 0]
+    return w2(perm_b32(bh, t, 0x05020100u), perm_b32(ah, bl, 0x07000601u));  // [b3 a4 b2 b5 | b1 a6 b0 a7]
 }
 
 RBX_HD uint64_t mul32x32(uint64_t x, uint64_t y) {  // (x & 0xffffffff) * (y >> 32)
     return (uint64_t)(uint32_t)x * (uint64_t)(uint32_t)(y >> 32);
 }
 
-// HighwayHash.java:93-114 update()
-RBX_HD void hh_update(HH &s, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3) {
-    s.v1[0] += s.mul0[0] + a0;
-    s.v1[1] += s.mul0[1] + a1;
-    s.v1[2] += s.mul0[2] + a2;
-    s.v1[3] += s.mul0[3] + a3;
+// HighwayHash.java:93-114 update(), after its first step (v1 += mul0 + a)
+RBX_HD void hh_update_tail(HH &s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         s.mul0[i] ^= mul32x32(s.v1[i], s.v0[i]);
@@ -184,10 +196,14 @@ RBX_HD void hh_update(HH &s, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3)
     s.v1[3] += zipper1(s.v0[3], s.v0[2]);
 }
 
-RBX_HD uint64_t w2(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// HighwayHash.java:93-114 update()
+RBX_HD void hh_update(HH &s, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3) {
+    s.v1[0] += s.mul0[0] + a0;
+    s.v1[1] += s.mul0[1] + a1;
+    s.v1[2] += s.mul0[2] + a2;
+    s.v1[3] += s.mul0[3] + a3;
+    hh_update_tail(s);
+}
 
 // streaming (read-once) vector loads of key bytes
 __device__ __forceinline__ uint4 ld_nt16(const void *p) {
@@ -216,11 +232,18 @@ RBX_HD void hh_remainder_prologue(HH &s, uint32_t r) {
     }
 }
 
-// permuteAndUpdate (:280-285) x6 and finalize128 (:186-198)
+// permuteAndUpdate (:280-285) x6 and finalize128 (:186-198).  permute() swaps the halves of
+// v0[2], v0[3], v0[0], v0[1]; the swapped words are added as halves with a carry.
 RBX_HD void hh_finalize128(HH &s, uint64_t &h1, uint64_t &h2) {
 #pragma unroll
-    for (int r = 0; r < 6; ++r)
-        hh_update(s, swap32c(s.v0[2]), swap32c(s.v0[3]), swap32c(s.v0[0]), swap32c(s.v0[1]));
+    for (int r = 0; r < 6; ++r) {
+        const uint64_t p0 = s.v0[2], p1 = s.v0[3], p2 = s.v0[0], p3 = s.v0[1];
+        s.v1[0] = add_halves(s.v1[0] + s.mul0[0], (uint32_t)(p0 >> 32), (uint32_t)p0);
+        s.v1[1] = add_halves(s.v1[1] + s.mul0[1], (uint32_t)(p1 >> 32), (uint32_t)p1);
+        s.v1[2] = add_halves(s.v1[2] + s.mul0[2], (uint32_t)(p2 >> 32), (uint32_t)p2);
+        s.v1[3] = add_halves(s.v1[3] + s.mul0[3], (uint32_t)(p3 >> 32), (uint32_t)p3);
+        hh_update_tail(s);
+    }
     h1 = s.v0[0] + s.mul0[0] + s.v1[2] + s.mul1[2];
     h2 = s.v0[1] + s.mul0[1] + s.v1[3] + s.mul1[3];
 }
