@@ -99,20 +99,23 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t sub = blockIdx.x % kBkSub;
     if (threadIdx.x < 128) s_cn[threadIdx.x] = 0;  // visible after the loop's first barrier
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
-        uint64_t h1[PER], h2[PER];
-        uint32_t w[PER], m[PER];
-        const uint64_t t0 = tile * TILE + threadIdx.x;
+    // Software-pipelined over tiles: tile t+1's hash and bit-0 gather are issued between tile
+    // t's bucket scan (whose reservation atomics are then in flight) and tile t's placement,
+    // so the VALU-heavy hash overlaps the reservation round trip and the gather has a whole
+    // placement + store phase to land.
+    uint64_t h1[PER], h2[PER];
+    uint32_t w[PER], m[PER];
+    auto hash_tile = [&](uint64_t tl) {
+        const uint64_t tt0 = tl * TILE + threadIdx.x;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const uint64_t t = t0 + q * NT;
+            const uint64_t t = tt0 + q * NT;
             h1[q] = h2[q] = 0;
             if (t < nchunk) bk_hash<KLEN>(keys, base + t, h1[q], h2[q]);
         }
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const uint64_t t = t0 + q * NT;
+            const uint64_t t = tt0 + q * NT;
             w[q] = 0;
             m[q] = 0;
             if (t < nchunk) {
@@ -121,6 +124,11 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
                 m[q] = bit_in_word(idx);
             }
         }
+    };
+    if ((uint64_t)blockIdx.x < ntiles) hash_tile(blockIdx.x);
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
+        const uint64_t t0 = tile * TILE + threadIdx.x;
         __syncthreads();  // s_cnt reset visible
         uint32_t idx[PER][KMAX - 1];
         bool surv[PER];
@@ -152,6 +160,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
             s_ncn[b] = tot - full;
             s_gb[b] = full ? atomicAdd(&cnt1[b * kBkSub + sub], full) : 0u;
         }
+        if (tile + gridDim.x < ntiles) hash_tile(tile + gridDim.x);  // the next tile (see above)
         __syncthreads();
         // the carried pairs go in front of their bucket's new ones
         for (uint32_t j = threadIdx.x; j < ncoarse * kBkLine1; j += NT) {
