@@ -76,14 +76,13 @@ constexpr uint32_t kBkLine1 = 8, kBkLine2 = 32;
 // LDS image and written out as one run per bucket (one global reservation per bucket per tile).
 template <int KMAX> constexpr int bk_per() { return KMAX <= 8 ? 2 : 1; }
 
-template <int KLEN, int KMAX, int NT>
+template <int KLEN, int KMAX, int NT, int PER>
 __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                    const uint32_t *__restrict__ bm, ModParams mp, uint32_t k,
                                                    uint32_t cshift, uint32_t ncoarse, uint64_t cap1,
                                                    unsigned long long *__restrict__ pairs1, uint32_t *__restrict__ cnt1,
                                                    unsigned long long *__restrict__ alive,
                                                    unsigned long long *__restrict__ miss, uint32_t flags) {
-    constexpr int PER = bk_per<KMAX>();
     constexpr int TILE = NT * PER;
     // dynamic LDS (bk_stage1_lds): image of a tile's pairs with each bucket's carried pairs in
     // front of its new ones, the bucket id of every image slot, the carries, the counters
@@ -269,7 +268,6 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                 e[2 * p] = w2(v[p].x, v[p].y);
                 e[2 * p + 1] = w2(v[p].z, v[p].w);
             }
-            if (start + TILE < nc) load(start + TILE);
             __syncthreads();
 #pragma unroll
             for (int p = 0; p < 2 * PER; ++p) {
@@ -277,14 +275,19 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                 if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
             }
             __syncthreads();
+            // the reservation atomics are issued here and their results stored to LDS only after
+            // the placement below, which overlaps their round trip (one 1024-thread block per CU:
+            // a blocking reservation idled the CU); the next tile's loads follow the atomics
+            uint32_t gb = 0;
             if (threadIdx.x < 64) bk_scan128(s_cnt, nf, s_start, s_pos);
             else if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) {
                 const uint32_t f = threadIdx.x - 128;
                 const uint32_t r = (c << fb) + f;
                 const uint32_t full = (s_cn[f] + s_cnt[f]) & ~(kBkLine2 - 1);
                 s_full[f] = full;
-                s_gb[f] = (full && r < nregions) ? atomicAdd(&cnt2[r], full) : 0u;
+                if (full && r < nregions) gb = atomicAdd(&cnt2[r], full);
             }
+            if (start + TILE < nc) load(start + TILE);
             __syncthreads();
 #pragma unroll
             for (int p = 0; p < 2 * PER; ++p) {
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                     s_img[slot] = e[p];
                 }
             }
+            if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) s_gb[threadIdx.x - 128] = gb;
             __syncthreads();
             for (uint32_t f = wave; f < nf; f += NT / 64) {
                 const uint32_t n = s_cnt[f], cn = s_cn[f], full = s_full[f], st = s_start[f];
@@ -532,14 +536,14 @@ __global__ __launch_bounds__(256) void k_bk_final(const unsigned long long *__re
 }
 
 // launcher -------------------------------------------------------------------------------
-template <int KLEN, int KMAX, int NT1>
+template <int KLEN, int KMAX, int NT1, int PER>
 static void bk_stage1(const PcArgs &a, hipStream_t st) {
-    constexpr int TILE = NT1 * bk_per<KMAX>();
+    constexpr int TILE = NT1 * PER;
     const uint64_t ntiles1 = (a.nchunk + TILE - 1) / TILE;
     const unsigned g1 = (unsigned)std::min<uint64_t>(ntiles1, 4096);
     const size_t nimg = (size_t)TILE * (a.k - 1) + 128 * (kBkLine1 - 1);
     const size_t lds1 = nimg * 8 + 128 * kBkLine1 * 8 + 7 * 128 * 4 + nimg;
-    hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX, NT1>), dim3(g1), dim3(NT1), lds1, st, a.keys, a.base, a.nchunk, a.bm,
+    hipLaunchKernelGGL((k_bk_stage1<KLEN, KMAX, NT1, PER>), dim3(g1), dim3(NT1), lds1, st, a.keys, a.base, a.nchunk, a.bm,
                        a.mp, a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
 }
 
@@ -554,10 +558,15 @@ static void bk_emit2(const PcArgs &a, hipStream_t st) {
 // LDS (one block per CU); 512 threads hold 67 KiB (two blocks per CU).
 static int g_emit2_nt = 1024;
 void set_contains_emit2_nt(int v) { g_emit2_nt = v; }
+// EXPERIMENTS (rbx_tune "contains_stage1_per"): keys per stage-1 thread for k <= 8 (2 = default:
+// 1024-key tiles, ~75 KiB of LDS, two blocks per CU; 1: 512-key tiles, three blocks per CU)
+static int g_stage1_per = 2;
+void set_contains_stage1_per(int v) { g_stage1_per = v; }
 
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
-    bk_stage1<KLEN, KMAX, 512>(a, st);
+    if (KMAX <= 8 && g_stage1_per == 1) bk_stage1<KLEN, KMAX, 512, 1>(a, st);
+    else bk_stage1<KLEN, KMAX, 512, bk_per<KMAX>()>(a, st);
     if (g_emit2_nt == 512) bk_emit2<512>(a, st);
     else bk_emit2<1024>(a, st);
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,

@@ -2651,6 +2651,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_qgrid(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "contains_stage1_per")) {
+        if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1_per in {1, 2}");
+        set_contains_stage1_per(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_emit2_nt")) {
         if (value != 512 && value != 1024) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024}");
         set_contains_emit2_nt(value);
