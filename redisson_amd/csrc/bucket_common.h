@@ -78,6 +78,32 @@ __device__ __forceinline__ void bk_scan128c(const uint32_t *cnt, const uint32_t 
     }
 }
 
+// bk_scan128c with every bucket's extent rounded up to a multiple of `al` slots (a power of two):
+// bucket starts are then aligned to whole output lines, so the 64-slot windows of a slot-linear
+// store never split a line between two store instructions
+__device__ __forceinline__ void bk_scan128c_al(const uint32_t *cnt, const uint32_t *car, uint32_t nb, uint32_t al,
+                                               uint32_t *start, uint32_t *pos) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ca = 2 * lane < nb ? car[2 * lane] : 0u, cb = 2 * lane + 1 < nb ? car[2 * lane + 1] : 0u;
+    const uint32_t a = ((2 * lane < nb ? cnt[2 * lane] : 0u) + ca + al - 1) & ~(al - 1);
+    const uint32_t b = ((2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u) + cb + al - 1) & ~(al - 1);
+    uint32_t x = a + b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    const uint32_t ex = x - a - b;
+    if (2 * lane < nb) {
+        start[2 * lane] = ex;
+        pos[2 * lane] = ex + ca;
+    }
+    if (2 * lane + 1 < nb) {
+        start[2 * lane + 1] = ex + a;
+        pos[2 * lane + 1] = ex + a + cb;
+    }
+}
+
 // the same for nb <= 256 (four buckets per lane)
 __device__ __forceinline__ void bk_scan256(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
     const uint32_t lane = threadIdx.x;

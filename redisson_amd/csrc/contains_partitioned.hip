@@ -87,6 +87,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
     // dynamic LDS (bk_stage1_lds): image of a tile's pairs with each bucket's carried pairs in
     // front of its new ones, the bucket id of every image slot, the carries, the counters
     extern __shared__ __attribute__((aligned(16))) unsigned char bk_lds[];
+    // new pairs + carries (<= 7 per bucket) + line rounding (<= 7 per bucket), ncoarse <= 64
     const uint32_t nimg = TILE * (k - 1) + 128 * (kBkLine1 - 1);
     unsigned long long *s_img = (unsigned long long *)bk_lds;   // [nimg]
     unsigned long long *s_car = s_img + nimg;                     // [128 * kBkLine1] carried pairs
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
             }
         }
         __syncthreads();
-        if (threadIdx.x < 64) bk_scan128c(s_cnt, s_cn, ncoarse, s_start, s_pos);
+        if (threadIdx.x < 64) bk_scan128c_al(s_cnt, s_cn, ncoarse, kBkLine1, s_start, s_pos);
         else if (threadIdx.x >= 128 && threadIdx.x - 128 < ncoarse) {
             const uint32_t b = threadIdx.x - 128;
             const uint32_t tot = s_cn[b] + s_cnt[b];
@@ -161,13 +162,16 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         }
         if (tile + gridDim.x < ntiles) hash_tile(tile + gridDim.x);  // the next tile (see above)
         __syncthreads();
-        // the carried pairs go in front of their bucket's new ones
+        // the carried pairs go in front of their bucket's new ones; the slots that round each
+        // bucket's extent up to a whole line are marked empty (0xff: ncoarse <= 64)
         for (uint32_t j = threadIdx.x; j < ncoarse * kBkLine1; j += NT) {
             const uint32_t b = j / kBkLine1, t = j % kBkLine1;
             if (t < s_cn[b]) {
                 s_img[s_start[b] + t] = s_car[j];
                 s_bkt[s_start[b] + t] = (uint8_t)b;
             }
+            const uint32_t tot = s_full[b] + s_ncn[b];
+            if (t < ((kBkLine1 - tot) & (kBkLine1 - 1))) s_bkt[s_start[b] + tot + t] = 0xff;
         }
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
@@ -191,6 +195,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         if (threadIdx.x < ncoarse) s_cn[threadIdx.x] = s_ncn[threadIdx.x];  // carries were placed above
         for (uint32_t i = threadIdx.x; i < total; i += NT) {
             const uint32_t b = s_bkt[i];
+            if (b == 0xffu) continue;  // alignment gap
             const uint32_t pos = i - s_start[b];
             const unsigned long long e = s_img[i];
             if (pos < s_full[b]) {
