@@ -229,7 +229,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
 // fine bucket = region within c.  Items are numbered c-minor so the blocks running at one time
 // reserve from different buckets' region counters.  Runs are whole lines (kBkLine2 pairs), the
 // remainder carries to the next tile (s_car), the item's last remainders are padded.
-template <int NT>
+template <int NT, int PER>
 __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
                                                   const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
                                                   uint32_t fb, uint32_t nregions, uint64_t cap2,
@@ -237,8 +237,8 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                                                   uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
                                                   uint32_t flags) {
-    constexpr int PER = 4;            // u32x4 (two pairs) per thread
-    constexpr uint32_t TILE = 8 * NT;
+    // PER u32x4 (two pairs each) per thread
+    constexpr uint32_t TILE = 2 * PER * NT;
     __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
     __shared__ unsigned long long s_car[128 * kBkLine2];
     __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128], s_full[128], s_cn[128];
@@ -552,16 +552,18 @@ static void bk_stage1(const PcArgs &a, hipStream_t st) {
                        a.mp, a.k, a.cshift, a.ncoarse, a.cap1, a.pairs1, a.cnt1, a.alive, a.miss, a.flags);
 }
 
-template <int NT2>
+template <int NT2, int PER>
 static void bk_emit2(const PcArgs &a, hipStream_t st) {
-    // one block per (coarse bucket, sub-partition); cap1 is a multiple of the 8 * NT2 tile
-    hipLaunchKernelGGL((k_bk_emit2<NT2>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1,
+    // one block per (coarse bucket, sub-partition); tiles start 16-byte aligned (cap1 is a multiple of 8192)
+    hipLaunchKernelGGL((k_bk_emit2<NT2, PER>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1,
                        a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
 }
 
-// EXPERIMENTS (rbx_tune "contains_emit2_nt"): emit2 workgroup size.  1024 threads hold 96 KiB of
-// LDS (one block per CU); 512 threads hold 67 KiB (two blocks per CU).
-static int g_emit2_nt = 1024;
+// EXPERIMENTS (rbx_tune "contains_emit2_nt"): emit2 shape.  1536 (default): 1024 threads, 12K-pair
+// tiles, 131 KiB of LDS, one block per CU; 1024: 8K-pair tiles (96 KiB; C2 4.84 -> 4.74 ms with 12K,
+// profiles/r02/r02u_abt_c2_emit2_tiles.jsonl); 1792: 14K-pair tiles; 512: 512 threads, 4K-pair tiles
+// (67 KiB, two blocks per CU).
+static int g_emit2_nt = 1536;
 void set_contains_emit2_nt(int v) { g_emit2_nt = v; }
 // EXPERIMENTS (rbx_tune "contains_stage1_per"): keys per stage-1 thread for k <= 8 (2 = default:
 // 1024-key tiles, ~75 KiB of LDS, two blocks per CU; 1: 512-key tiles, three blocks per CU)
@@ -572,8 +574,10 @@ template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
     if (KMAX <= 8 && g_stage1_per == 1) bk_stage1<KLEN, KMAX, 512, 1>(a, st);
     else bk_stage1<KLEN, KMAX, 512, bk_per<KMAX>()>(a, st);
-    if (g_emit2_nt == 512) bk_emit2<512>(a, st);
-    else bk_emit2<1024>(a, st);
+    if (g_emit2_nt == 512) bk_emit2<512, 4>(a, st);
+    else if (g_emit2_nt == 1024) bk_emit2<1024, 4>(a, st);  // 8K-pair tiles
+    else if (g_emit2_nt == 1792) bk_emit2<1024, 7>(a, st);  // 14K-pair tiles
+    else bk_emit2<1024, 6>(a, st);                          // 12K-pair tiles (default)
     hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
                        a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges, a.flags);
     hipLaunchKernelGGL(k_bk_misses, dim3(2048), dim3(1024), 0, st, a.mrec, a.mcnt, a.capm, a.nmranges, a.miss);

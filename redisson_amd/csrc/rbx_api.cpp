@@ -2657,7 +2657,8 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     if (!strcmp(key, "contains_emit2_nt")) {
-        if (value != 512 && value != 1024) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024}");
+        if (value != 512 && value != 1024 && value != 1536 && value != 1792)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024, 1536, 1792}");
         set_contains_emit2_nt(value);
         return RBX_OK;
     }
