@@ -448,6 +448,27 @@ def run_c2(args, world, rank, local):
     L.lib().rbx_tune(b"contains_partition", 2)
     direct_ms = t_dir.ms / 3
     assert int(cnt[3].item()) == 4 * (total_present // args.steps), "direct and partitioned counts differ"
+    # SURVEY 8(d) C2's second filter: tryInit(448_089_842, 0.01) -> m = 4,294,967,293 bits, k = 7
+    # (not a power of two: the exact 63-bit modulo instead of a mask), the same keys
+    fn = client.getBloomFilter("bench-c2-tryinit")
+    assert fn.tryInit(448_089_842, 0.01)
+    assert fn.getSize() == 4_294_967_293 and fn.getHashIterations() == K
+    hn = BloomHandle(client, "bench-c2-tryinit")
+    cnt.zero_()
+    torch.cuda.synchronize()
+    with Timer(stream) as t_addn:
+        hn.add_dev(device_keys(added.data_ptr(), half, 32), cnt.data_ptr(), stream=sptr)
+    hn.contains_dev(dk, cnt.data_ptr() + 8, stream=sptr)
+    with Timer(stream) as t_conn:
+        for _ in range(3):
+            hn.contains_dev(dk, cnt.data_ptr() + 16, stream=sptr)
+    assert int(cnt[2].item()) == 3 * int(cnt[1].item()) and int(cnt[1].item()) >= half
+    nonpow2 = {"size_bits": 4_294_967_293, "k": K, "tryInit": [448_089_842, 0.01],
+               "add_ms": t_addn.ms, "add_keys_per_s_per_gpu": half / (t_addn.ms / 1e3),
+               "contains_ms": t_conn.ms / 3, "contains_keys_per_s_per_gpu": n / (t_conn.ms / 3 / 1e3),
+               "present_per_step": int(cnt[1].item())}
+    hn.close()
+    fn.delete()
     hostpath = None if args.no_hostpath or rank != 0 else host_path_rate(client, "bench-c2")
 
     step_s = max_over_ranks(world, max(kern_ms / 1e3, 0.0))
@@ -472,7 +493,7 @@ def run_c2(args, world, rank, local):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      # one contains call = the partitioned pipeline's kernels in sequence on one stream
-                     "kernel": "contains pipeline: k_bk_stage1<32,8,512> + k_bk_emit2<1024> + k_bk_probe + "
+                     "kernel": "contains pipeline: k_bk_stage1<32,8,512,2> + k_bk_emit2<1024,6> + k_bk_probe + "
                                "k_bk_misses + k_bk_final",
                      "kernel_avg_ms": kern_ms,
                      # the pipeline's own floor: keys + bitmap streamed once (3.74 GB per call)
@@ -497,7 +518,8 @@ def run_c2(args, world, rank, local):
                   "add_traffic": load_traffic(args.traffic_json, "add_pipeline", "hbm_bytes_by_class") or
                   load_traffic(args.traffic_json, "add_pipeline"),
                   "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch"),
-                  "host_path": hostpath},
+                  "host_path": hostpath,
+                  "c2_tryinit_nonpow2": nonpow2},
     }
     h.close()
     f.delete()
