@@ -120,8 +120,10 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
             m[q] = 0;
             if (t < nchunk) {
                 const uint32_t idx = mod63(h1[q] & 0x7fffffffffffffffULL, mp);
-                w[q] = bm[idx >> 5];
                 m[q] = bit_in_word(idx);
+                // diagnostics (flags 32, wrong answers): no bit-0 gather; ~54% of keys survive
+                if (flags & 32) w[q] = (uint32_t)(h2[q] >> 40) % 100u < 54u ? m[q] : 0u;
+                else w[q] = bm[idx >> 5];
             }
         }
     };

@@ -2603,8 +2603,8 @@ int rbx_tune(const char *key, int value) {
     // DIAGNOSTICS ONLY (tools/microbench.py pflags), results become wrong: 4 = stage 1 emits no
     // pairs, 8 = the probe records no misses.  0 = normal operation.
     if (!strcmp(key, "contains_partition_flags")) {
-        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16}");
+        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16 && value != 32)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16, 32}");
         g_partition_flags = value;
         return RBX_OK;
     }

@@ -467,7 +467,7 @@ def main():
                 L.lib().rbx_tune(b"contains_partition_flags", fl)
                 cnt[1].zero_()
                 res[(mode, fl)].append(timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 8, stream=sp), 2))
-                if not fl & 12:
+                if not fl & 44:
                     counts[(mode, fl)] = int(cnt[1].item())
         assert len(set(counts.values())) == 1, counts
         for (mode, fl), v in res.items():
