@@ -160,18 +160,14 @@ RBX_HD uint64_t add_halves(uint64_t x, uint32_t lo, uint32_t hi) {
 // zipperMerge0/1 (HighwayHash.java:248-260).  With a = lower-lane operand (Java's "v0"
 // parameter) and b = upper (Java's "v1"), byte j of the result:
 //   zm0 = [a3 b4 a2 a5 | b6 a1 b7 a0]      zm1 = [b3 a4 b2 b5 | b1 a6 b0 a7]
-// Three byte permutes each: the low word needs three source words (two perms), the high
-// word two (one perm).
-RBX_HD uint64_t zipper0(uint64_t b, uint64_t a) {
-    const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bh = (uint32_t)(b >> 32);
-    const uint32_t t = perm_b32(bh, al, 0x0C020403u);                           // [a3 b4 a2 0]
-    return w2(perm_b32(ah, t, 0x05020100u), perm_b32(bh, al, 0x00070106u));  // [a3 b4 a2 a5 | b6 a1 b7 a0]
-}
-
-RBX_HD uint64_t zipper1(uint64_t b, uint64_t a) {
-    const uint32_t ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
-    const uint32_t t = perm_b32(ah, bl, 0x0C020403u);                           // [b3 a4 b2 0]
-    return w2(perm_b32(bh, t, 0x05020100u), perm_b32(ah, bl, 0x07000601u));  // [b3 a4 b2 b5 | b1 a6 b0 a7]
+// Each high word is one byte permute (v_perm_b32) of two source words; each low word needs three
+// source words, but both low words take their two bytes from {a4 a5 b4 b5}, gathered once as
+// X = [b4 a5 b5 a4]: the pair costs five permutes instead of six.
+RBX_HD void zipper_pair(uint64_t b, uint64_t a, uint64_t &z0, uint64_t &z1) {
+    const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint32_t x = perm_b32(ah, bh, 0x04010500u);                                // [b4 a5 b5 a4]
+    z0 = w2(perm_b32(x, al, 0x05020403u), perm_b32(bh, al, 0x00070106u));  // [a3 b4 a2 a5 | b6 a1 b7 a0]
+    z1 = w2(perm_b32(x, bl, 0x06020703u), perm_b32(ah, bl, 0x07000601u));  // [b3 a4 b2 b5 | b1 a6 b0 a7]
 }
 
 RBX_HD uint64_t mul32x32(uint64_t x, uint64_t y) {  // (x & 0xffffffff) * (y >> 32)
@@ -186,14 +182,19 @@ RBX_HD void hh_update_tail(HH &s) {
         s.v0[i] += s.mul1[i];
         s.mul1[i] ^= mul32x32(s.v0[i], s.v1[i]);
     }
-    s.v0[0] += zipper0(s.v1[1], s.v1[0]);
-    s.v0[1] += zipper1(s.v1[1], s.v1[0]);
-    s.v0[2] += zipper0(s.v1[3], s.v1[2]);
-    s.v0[3] += zipper1(s.v1[3], s.v1[2]);
-    s.v1[0] += zipper0(s.v0[1], s.v0[0]);
-    s.v1[1] += zipper1(s.v0[1], s.v0[0]);
-    s.v1[2] += zipper0(s.v0[3], s.v0[2]);
-    s.v1[3] += zipper1(s.v0[3], s.v0[2]);
+    uint64_t z0, z1, z2, z3;
+    zipper_pair(s.v1[1], s.v1[0], z0, z1);
+    zipper_pair(s.v1[3], s.v1[2], z2, z3);
+    s.v0[0] += z0;
+    s.v0[1] += z1;
+    s.v0[2] += z2;
+    s.v0[3] += z3;
+    zipper_pair(s.v0[1], s.v0[0], z0, z1);
+    zipper_pair(s.v0[3], s.v0[2], z2, z3);
+    s.v1[0] += z0;
+    s.v1[1] += z1;
+    s.v1[2] += z2;
+    s.v1[3] += z3;
 }
 
 // HighwayHash.java:93-114 update()
