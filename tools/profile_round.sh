@@ -19,9 +19,10 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o p -- python3 $B > "$OUT/pmc_write.log" 2>&1 || exit 1
 timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmc_tcc" -o p -- python3 $B > "$OUT/pmc_tcc.log" 2>&1 || exit 1
 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace --output-format csv -d "$OUT/pmc_req" -o p -- python3 $B > "$OUT/pmc_req.log" 2>&1 || exit 1
-# API calls per bench run: warmup 2 + steps 5 of the measured op; C2 also adds twice (scratch warm-up + setup)
+# API calls per bench run: warmup 2 + steps 5 of the measured op; C2 also adds twice (scratch warm-up + setup),
+# and its tryInit(448_089_842, 0.01) filter adds once and contains 4 times (extra.c2_tryinit_nonpow2)
 python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/pmc_req" -o "$OUT/traffic.json" \
-  --calls contains_pipeline=7 add_pipeline=2 stream_pipeline=7 --stream-bytes $SB > /dev/null || exit 1
+  --calls contains_pipeline=11 add_pipeline=3 stream_pipeline=7 --stream-bytes $SB > /dev/null || exit 1
 # keep summaries only (gpurun copies back <= 64 MiB): stats CSVs, our kernels' counter rows
 for d in pmc_fetch pmc_write pmc_tcc pmc_req; do
   f=$(find "$OUT/$d" -name "*counter_collection.csv" | head -1)
