@@ -43,6 +43,15 @@ constexpr uint32_t kBaRegionWords = 1u << (kBaRegionBits - 5);  // 2048
 // runs with LDS carries, as in contains_partitioned.hip, measured slower here: stage A 2.09 ->
 // 2.61 ms, the rebucket 2.10 -> 2.42 ms, 50M C2 keys.)
 
+// Runs of the two radix passes are written with plain (L2 write-back) stores, not the
+// nontemporal ones the contains pipeline uses: these runs are not whole lines, and the partial
+// line at the end of one block's run and the start of the next reservation's (a block of the
+// same sub-partition, blockIdx % 16, so the same XCD's L2 under round-robin dispatch) merge in
+// L2 before write-back.  Measured (50M C2 keys): stage-1 write requests 72.6M -> 56.9M, rebucket
+// 52.7M -> 49.8M, add 5.01 -> 4.83 ms; the contains pipeline, whose runs are whole lines, was
+// 4.64 -> 4.84 ms slower with plain stores (profiles/r02/r02z_plain_stores.txt).
+template <class T> __device__ __forceinline__ void ba_run_store(T v, T *p) { *p = v; }
+
 // A ------------------------------------------------------------------------------------
 template <int KMAX> constexpr int ba_per() { return KMAX <= 8 ? 2 : 1; }
 
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
         for (uint32_t i = threadIdx.x; i < total; i += NT) {
             const uint32_t b = s_bkt[i];
             const uint64_t gp = (uint64_t)s_gb[b] + (i - s_start[b]);
-            if (gp < cap1) run_store(s_img[i], p1 + (uint64_t)(b * kBkSub + sub) * cap1 + gp);
+            if (gp < cap1) ba_run_store(s_img[i], p1 + (uint64_t)(b * kBkSub + sub) * cap1 + gp);
             else *overflow = 1u;
         }
         __syncthreads();  // LDS reuse
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
         for (uint32_t i = threadIdx.x; i < m; i += NT) {
             const uint32_t f = s_bkt[i];
             const uint64_t gp = (uint64_t)s_gb[f] + (i - s_start[f]);
-            if (gp < cap_out) run_store(s_img[i], pout + (uint64_t)((parent << fo) + f) * cap_out + gp);
+            if (gp < cap_out) ba_run_store(s_img[i], pout + (uint64_t)((parent << fo) + f) * cap_out + gp);
             else *overflow = 1u;
         }
         __syncthreads();
