@@ -919,15 +919,24 @@ def main():
         ls, lw = min(args.steps, args.leg_steps), min(args.warmup, 2)
         res["legs"] = {}
         for leg in legs:
-            log(f"[bench] rank {rank} leg {leg}")
-            if leg == "c1":
-                res["legs"]["c1"] = run_c1(args, world, rank, local)
-            elif leg == "c3":
-                res["legs"]["c3"] = run_c3(args, world, rank, local, ls, lw)
-            elif leg == "c4":
-                res["legs"]["c4"] = run_c4(args, world, rank, local, ls, lw)
-            else:
+            if leg not in ("c1", "c3", "c4"):
                 raise SystemExit(f"unknown leg {leg}")
+        for leg in legs:
+            log(f"[bench] rank {rank} leg {leg}")
+            # a leg that raises (on every rank alike, e.g. a failed RCCL init) is reported in the
+            # line instead of taking the C2 headline down with it
+            try:
+                if leg == "c1":
+                    res["legs"]["c1"] = run_c1(args, world, rank, local)
+                elif leg == "c3":
+                    res["legs"]["c3"] = run_c3(args, world, rank, local, ls, lw)
+                else:
+                    res["legs"]["c4"] = run_c4(args, world, rank, local, ls, lw)
+            except Exception as e:  # noqa: BLE001
+                import traceback
+
+                traceback.print_exc()
+                res["legs"][leg] = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     elif args.workload == "c4":
