@@ -227,7 +227,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
 }
 
 // K3 -----------------------------------------------------------------------------------
-// One block per (coarse bucket c, sub-partition) work item, over its 8192-pair tiles in order;
+// One block per (coarse bucket c, sub-partition) work item, over its 2*PER*NT-pair tiles in order;
 // fine bucket = region within c.  Items are numbered c-minor so the blocks running at one time
 // reserve from different buckets' region counters.  Runs are whole lines (kBkLine2 pairs), the
 // remainder carries to the next tile (s_car), the item's last remainders are padded.
