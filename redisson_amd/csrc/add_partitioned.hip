@@ -101,10 +101,11 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
             }
         }
         __syncthreads();
+        uint32_t gb = 0;
         if (threadIdx.x < 64) bk_scan256(s_cnt, ncoarse, s_start, s_pos);
         else if (threadIdx.x >= 256 && threadIdx.x - 256 < ncoarse) {
             const uint32_t b = threadIdx.x - 256;
-            s_gb[b] = s_cnt[b] ? atomicAdd(&cnt1[b * kBkSub + sub], s_cnt[b]) : 0u;
+            if (s_cnt[b]) gb = atomicAdd(&cnt1[b * kBkSub + sub], s_cnt[b]);
         }
         __syncthreads();
 #pragma unroll
@@ -122,6 +123,8 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
                 }
             }
         }
+        // reservation results stored after the placement, which overlapped their round trip
+        if (threadIdx.x >= 256 && threadIdx.x - 256 < ncoarse) s_gb[threadIdx.x - 256] = gb;
         __syncthreads();
         const uint32_t total = (uint32_t)min<uint64_t>(TILE, nchunk - tile * TILE) * f.k;
         for (uint32_t i = threadIdx.x; i < total; i += NT) {
@@ -191,11 +194,12 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
             if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u);
         }
         __syncthreads();
+        uint32_t gb = 0;
         if (threadIdx.x < 64) bk_scan256(s_cnt, nf, s_start, s_pos);
         else if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) {
             const uint32_t f = threadIdx.x - 256;
             const uint32_t r = (parent << fo) + f;
-            s_gb[f] = (s_cnt[f] && r < nparts_out) ? atomicAdd(&cnt_out[r], s_cnt[f]) : 0u;
+            if (s_cnt[f] && r < nparts_out) gb = atomicAdd(&cnt_out[r], s_cnt[f]);
         }
         __syncthreads();
 #pragma unroll
@@ -208,6 +212,8 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
                 s_bkt[slot] = (uint8_t)f;
             }
         }
+        // the reservation results reach LDS only now: the placement above overlapped their round trip
+        if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) s_gb[threadIdx.x - 256] = gb;
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < m; i += NT) {
             const uint32_t f = s_bkt[i];
