@@ -128,10 +128,10 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         }
     };
     if ((uint64_t)blockIdx.x < ntiles) hash_tile(blockIdx.x);
+    if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;  // later tiles: reset during the placement
+    __syncthreads();
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         const uint64_t t0 = tile * TILE + threadIdx.x;
-        __syncthreads();  // s_cnt reset visible
         uint32_t idx[PER][KMAX - 1];
         bool surv[PER];
 #pragma unroll
@@ -164,6 +164,9 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
         }
         if (tile + gridDim.x < ntiles) hash_tile(tile + gridDim.x);  // the next tile (see above)
         __syncthreads();
+        // s_cnt was last read by the scan and the reservations above: reset for the next tile
+        // (visible to its counting after this tile's last barrier)
+        if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
         // the carried pairs go in front of their bucket's new ones; the slots that round each
         // bucket's extent up to a whole line are marked empty (0xff: ncoarse <= 64)
         for (uint32_t j = threadIdx.x; j < ncoarse * kBkLine1; j += NT) {
@@ -243,14 +246,20 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
     constexpr uint32_t TILE = 2 * PER * NT;
     __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
     __shared__ unsigned long long s_car[128 * kBkLine2];
-    __shared__ uint32_t s_cnt[128], s_start[128], s_pos[128], s_gb[128], s_full[128], s_cn[128];
+    // s_cnt is double-buffered: a tile counts into one buffer while the other (read by the previous
+    // tile's stores) is cleared, which saves the barrier a reset at the top of the tile needed
+    __shared__ uint32_t s_cnt2[2][128], s_start[128], s_pos[128], s_gb[128], s_full[128], s_cn[128];
     const uint32_t nf = 1u << fb, fmask = nf - 1;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t nparts = ncoarse * kBkSub;
     for (uint32_t item = blockIdx.x; item < nparts; item += gridDim.x) {
         const uint32_t c = item % ncoarse, cs = c * kBkSub + item / ncoarse;
         const uint64_t nc = min<uint64_t>(cnt1[cs], cap1);
-        if (threadIdx.x < 128) s_cn[threadIdx.x] = 0;
+        if (threadIdx.x < 128) {
+            s_cn[threadIdx.x] = 0;
+            s_cnt2[0][threadIdx.x] = 0;
+        }
+        uint32_t par = 0;
         // an item with no pairs goes straight to the remainder loop, whose waves read the
         // counters zeroed above by waves 0-1: LDS holds the previous kernel's bytes otherwise
         __syncthreads();
@@ -268,14 +277,14 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
         if (nc) load(0);
         for (uint64_t start = 0; start < nc; start += TILE) {
             const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
-            if (threadIdx.x < 128) s_cnt[threadIdx.x] = 0;
+            uint32_t *s_cnt = s_cnt2[par];
+            if (threadIdx.x < 128) s_cnt2[par ^ 1][threadIdx.x] = 0;  // the next tile's (visible after this tile's last barrier)
             unsigned long long e[2 * PER];
 #pragma unroll
             for (int p = 0; p < PER; ++p) {
                 e[2 * p] = w2(v[p].x, v[p].y);
                 e[2 * p + 1] = w2(v[p].z, v[p].w);
             }
-            __syncthreads();
 #pragma unroll
             for (int p = 0; p < 2 * PER; ++p) {
                 const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
@@ -321,6 +330,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                 }
                 if (lane == 0) s_cn[f] = cn + n - full;
             }
+            par ^= 1u;
             __syncthreads();
         }
         for (uint32_t f = wave; f < nf; f += NT / 64) {  // the item's last remainders, padded
