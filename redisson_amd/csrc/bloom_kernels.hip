@@ -1260,6 +1260,14 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
 
 static int g_stream_slots = 0;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel
 void set_stream_slots(int v) { g_stream_slots = v; }
+// k_stream_contains runs best at four 256-thread blocks per CU (4 waves/SIMD): the Zipf-hot
+// tenants' bitmaps live in L2, and more resident waves interleave more tenants.  Its registers
+// (93 VGPRs since the r02 hash) would admit five, so the launch reserves 33,000 bytes of dynamic
+// LDS per block (four fit in 160 KiB).  C5, same box: 11.28 -> 10.99 ms per 1e8 commands; three
+// blocks per CU: 0.66 ms per chunk vs 0.545 (profiles/r02/r02ze_c5_occupancy.txt).
+// rbx_tune("stream_contains_lds") overrides the bytes (0: registers decide).
+static int g_stream_lds = 33000;
+void set_stream_contains_lds(int v) { g_stream_lds = v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1274,7 +1282,7 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                            a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out,
                            a.counts);
     else
-        hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk,
+        hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out, a.counts);
     hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);

@@ -2651,6 +2651,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_qgrid(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "stream_contains_lds")) {
+        if (value < 0 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_contains_lds in [0, 65536]");
+        set_stream_contains_lds(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_stage1_per")) {
         if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1_per in {1, 2}");
         set_contains_stage1_per(value);
