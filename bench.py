@@ -256,12 +256,42 @@ def stream_read_peak(client, nbytes, stream):
     return nbytes / (t.ms / 5 / 1e3) / 1e9
 
 
-def request_fields(traffic_json, kernel, ms, peak):
-    """PMC memory requests per launch (TCC_EA0_RDREQ + WRREQ, profiles/traffic.json) vs a request
-    peak measured at the same working set and locality."""
+def stream_write_peak(client, nbytes, stream):
+    """HBM stream-write rate (16-byte nontemporal stores over an nbytes buffer) in 64-byte write
+    requests per second: the write side of the request roofline."""
+    import torch
+
+    from redisson_amd import _lib as L
+
+    sptr = stream.cuda_stream
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    L.lib().rbx_bench_stream_write(client.ctx, buf.data_ptr(), nbytes, sptr)
+    with Timer(stream) as t:
+        for _ in range(5):
+            L.lib().rbx_bench_stream_write(client.ctx, buf.data_ptr(), nbytes, sptr)
+    del buf
+    return nbytes / 64 / (t.ms / 5 / 1e3)
+
+
+def request_fields(traffic_json, kernel, ms, peak, write_peak=None):
+    """PMC memory requests per launch (TCC_EA0_RDREQ + WRREQ, profiles/traffic.json) against the
+    request rates measured in the same run: reads at `peak` (random gathers at the same working set
+    and locality -- above the streaming-read request rate), writes at `write_peak` (whole 64-byte
+    streaming writes).  request_frac = (reads / peak + writes / write_peak) / call time: the share
+    of the call a request-bound design needs at those rates."""
     reqs = load_traffic(traffic_json, kernel, "requests_per_launch")
-    return {"requests_per_launch": reqs, "request_rate_per_s": reqs / (ms / 1e3) if reqs else None,
-            "request_peak_per_s": peak, "request_frac": reqs / (ms / 1e3) / peak if reqs and peak else None}
+    rd = load_traffic(traffic_json, kernel, "read_requests_per_launch")
+    wr = load_traffic(traffic_json, kernel, "write_requests_per_launch")
+    out = {"requests_per_launch": reqs, "request_rate_per_s": reqs / (ms / 1e3) if reqs else None,
+           "request_peak_per_s": peak, "read_requests_per_launch": rd, "write_requests_per_launch": wr,
+           "write_request_peak_per_s": write_peak}
+    if rd is not None and wr is not None and peak and write_peak:
+        floor_s = rd / peak + wr / write_peak
+        out["request_floor_ms"] = floor_s * 1e3
+        out["request_frac"] = floor_s / (ms / 1e3)
+    else:
+        out["request_frac"] = reqs / (ms / 1e3) / peak if reqs and peak else None
+    return out
 
 
 # ------------------------------------------------------------------------------------------
@@ -422,6 +452,7 @@ def run_c2(args, world, rank, local):
     present_one = int(cnt[1].item()) // max(args.warmup, 1) if args.warmup else None
 
     gathers_per_s = gather_peak(client, SIZE // 8, n, K, stream, g)  # same 512 MiB working set
+    writes_per_s = stream_write_peak(client, 2 << 30, stream)
 
     # timed region
     cnt[2].zero_()
@@ -479,7 +510,7 @@ def run_c2(args, world, rank, local):
     floor_bytes = n * 32 + SIZE // 8  # what any streaming design must move: the keys and the bitmap once
     traffic = load_traffic(args.traffic_json, "contains_pipeline", "hbm_bytes_by_class") or \
         load_traffic(args.traffic_json, "contains_pipeline")
-    reqs = load_traffic(args.traffic_json, "contains_pipeline", "requests_per_launch")
+    reqf = request_fields(args.traffic_json, "contains_pipeline", kern_ms, gathers_per_s, writes_per_s)
     res = {
         "metric": "Bloom contains keys/sec (whole node), C2: one 2^32-bit filter, k=7, 32-byte keys",
         "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -501,11 +532,9 @@ def run_c2(args, world, rank, local):
                                          "achieved": floor_bytes / (kern_ms / 1e3) / 1e9,
                                          "frac": floor_bytes / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
                      # the binding limit: memory requests at the L2->EA interface (PMC TCC_EA0_RD/WRREQ),
-                     # against the measured random-gather request rate at this working set
-                     "requests_per_launch": reqs,
-                     "request_rate_per_s": (reqs / (kern_ms / 1e3)) if reqs else None,
-                     "request_peak_per_s": gathers_per_s,
-                     "request_frac": (reqs / (kern_ms / 1e3) / gathers_per_s) if reqs else None,
+                     # reads against the measured random-gather request rate at this working set,
+                     # writes against the measured streaming-write request rate
+                     **reqf,
                      # north-star definition: keys/s x k / measured random-gather peak at this
                      # working set (> 1: early exit and LDS probes avoid most random gathers)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
@@ -664,7 +693,7 @@ def run_c3(args, world, rank, local, steps, warmup):
                      load_traffic(args.traffic_json, kname),
                      "kernel": kdesc, "kernel_avg_ms": ms,
                      "request_peak_kind": "k_gather_segments: 4 random loads per key inside its tenant's slice",
-                     **request_fields(args.traffic_json, kname, ms, peak)},
+                     **request_fields(args.traffic_json, kname, ms, peak, stream_write_peak(client, 1 << 30, stream))},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
     for h in handles:
@@ -737,7 +766,10 @@ def run_c5(args, world, rank, local):
     top = int(torch.bincount(kf.long(), minlength=nt).max().item())
     del pool
     tbl = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
-    peak = segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), 1_797_199, 1, n, stream)
+    # read-request peak: the larger of the tenant-slice gather rate (uniform tenants, one key per
+    # slice) and the uniform 512 MiB gather rate -- Zipf-hot tenants gather above the former
+    peak = max(segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), 1_797_199, 1, n, stream),
+               gather_peak(client, 512 << 20, n, 7, stream, g))
     del tbl
     algo = n * (64 + 10 * 8)
     res = {
@@ -755,9 +787,10 @@ def run_c5(args, world, rank, local):
                      "traffic": load_traffic(args.traffic_json, "stream_pipeline", "hbm_bytes_by_class") or
                      load_traffic(args.traffic_json, "stream_pipeline"),
                      "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms,
-                     "request_peak_kind": "k_gather_segments, one key per tenant slice (uniform tenants: "
-                                          "no Zipf reuse, a lower bound on C5's locality)",
-                     **request_fields(args.traffic_json, "stream_pipeline", ms, peak)},
+                     "request_peak_kind": "max(k_gather_segments one key per tenant slice, k_gather_probe "
+                                          "over 512 MiB) for reads; k_stream_write for writes",
+                     **request_fields(args.traffic_json, "stream_pipeline", ms, peak,
+                                      stream_write_peak(client, 1 << 30, stream))},
     }
     for h in handles:
         h.close()

@@ -24,6 +24,9 @@ int rbx_bench_slice_probe(rbx_ctx *ctx, const void *d_entries, uint64_t per_buck
                           const void *d_bitmap, uint64_t slice_bytes, unsigned grid, void *d_sink, void *stream);
 /* Stream-read roofline probe: reads `bytes` (16-byte aligned buffer) with 16-byte loads. */
 int rbx_bench_stream_read(rbx_ctx *ctx, const void *d_buf, uint64_t bytes, void *d_sink, void *stream);
+/* Stream-write roofline probe: writes `bytes` (16-byte aligned buffer) with 16-byte nontemporal
+ * stores (whole 64-byte write requests). */
+int rbx_bench_stream_write(rbx_ctx *ctx, void *d_buf, uint64_t bytes, void *stream);
 /* Segment-local gather probe (the locality of a multi-tenant batch): key i belongs to segment
  * i / keys_per_segment, a consecutive segment_bytes slice of the table (wrapping), and does 4
  * random 4-byte loads inside it. */

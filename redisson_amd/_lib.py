@@ -167,6 +167,7 @@ SIGNATURES = {
     "rbx_node_hll_merge": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
     "rbx_bench_slice_probe": (C.c_int, [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint, vp, vp]),
     "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
+    "rbx_bench_stream_write": (C.c_int, [vp, vp, C.c_uint64, vp]),
     "rbx_bench_gather_segments": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp]),
     # binary names (rbx_name)
     "rbx_bloom_try_init_n": (C.c_int, [vp, RbxName, C.c_int64, C.c_double, C.POINTER(C.c_int)]),

@@ -1440,6 +1440,20 @@ void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStre
     hipLaunchKernelGGL(k_stream_read, dim3(4096), dim3(256), 0, st, (const u32x4 *)buf, bytes / 16, sink);
 }
 
+// Streaming-write roofline probe: 16-byte nontemporal stores over a whole buffer (whole 64-byte
+// write requests, the form the partition passes' runs take).
+__global__ __launch_bounds__(256) void k_stream_write(u32x4 *__restrict__ dst, uint64_t n16, uint32_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint32_t x = (uint32_t)i ^ seed;
+        __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + i);
+    }
+}
+
+void launch_stream_write(void *buf, uint64_t bytes, hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_write, dim3(4096), dim3(256), 0, st, (u32x4 *)buf, bytes / 16, 0x9E3779B9u);
+}
+
 // Slice-probe roofline: the bitmap is cut into nbuckets slices of 2^slice_log2 bytes; bucket b's
 // entries (8 bytes: word offset in the slice, payload) are streamed and each tests one word of
 // slice b.  Workgroup w takes the buckets w % 8, w % 8 + 8, ... (blocks b and b + 8 share an XCD

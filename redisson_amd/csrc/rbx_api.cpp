@@ -2487,6 +2487,14 @@ int rbx_bench_stream_read(rbx_ctx *c, const void *d_buf, uint64_t bytes, void *d
     return RBX_OK;
 }
 
+int rbx_bench_stream_write(rbx_ctx *c, void *d_buf, uint64_t bytes, void *stream) {
+    if (!c || !d_buf || ((uintptr_t)d_buf & 15)) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    RBX_TRY(set_device(c));
+    launch_stream_write(d_buf, bytes, pick_stream(c, stream));
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
 int rbx_bench_gather_segments(rbx_ctx *c, const void *d_table, uint64_t table_bytes, uint64_t segment_bytes,
                               uint64_t keys_per_segment, uint64_t nkeys, void *d_sink, void *stream) {
     if (!c || !d_table || !d_sink || segment_bytes < 4 || table_bytes < segment_bytes || !keys_per_segment)

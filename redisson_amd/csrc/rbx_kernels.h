@@ -162,6 +162,7 @@ void launch_bench_slice_probe(const void *ent, uint64_t per_bucket, uint32_t nbu
                               uint32_t slice_words_log2, unsigned grid, uint32_t *sink, hipStream_t st);
 // streaming 16-byte reads of a whole buffer: the HBM stream-read roofline probe
 void launch_stream_read(const void *buf, uint64_t bytes, uint32_t *sink, hipStream_t st);
+void launch_stream_write(void *buf, uint64_t bytes, hipStream_t st);
 // random 4-byte gathers (k per key, nkeys keys) over an nwords-word table: roofline probe
 void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, uint32_t k, uint32_t *sink,
                          hipStream_t st);

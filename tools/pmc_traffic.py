@@ -100,6 +100,8 @@ def main():
         if "TCC_EA0_RDREQ_sum" in cs and "TCC_EA0_WRREQ_sum" in cs:
             # memory requests at the L2 -> EA interface (the binding rate for these kernels)
             e["requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"] + cs["TCC_EA0_WRREQ_sum"]
+            e["read_requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"]
+            e["write_requests_per_launch"] = cs["TCC_EA0_WRREQ_sum"]
         rd = cs.get("TCC_EA0_RDREQ_sum")
         if rd is None and fetch is not None:
             rd = fetch * 1024 / 64  # FETCH_SIZE = RDREQ x 64 B
@@ -129,8 +131,8 @@ def main():
         agg = {"kernels": list(parts), "calls_profiled": calls[name],
                "note": "per API call: sum over the profiled launches / calls (the keys "
                        "written '_per_launch' here mean per call)"}
-        for f in ("hbm_bytes_per_launch", "hbm_bytes_by_class", "requests_per_launch", "fetch_bytes_x2",
-                  "write_bytes"):
+        for f in ("hbm_bytes_per_launch", "hbm_bytes_by_class", "requests_per_launch", "read_requests_per_launch",
+                  "write_requests_per_launch", "fetch_bytes_x2", "write_bytes"):
             if all(f in out[k] for k in parts):
                 agg[f] = sum(out[k][f] * launches[k] for k in parts) / calls[name]
         out[name] = agg
