@@ -47,7 +47,14 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *                           2 auto (default: the call's bitmaps exceed 64 MiB)
  *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44
  *   "contains_qgrid"        slot kernel grid, 256..8192 (default 2048)
- *   "stream_contains_slots" ordered-stream contains: 0 staged kernel (default), 1 slot kernel */
+ *   "stream_contains_slots" ordered-stream contains: 0 staged kernel (default), 1 slot kernel
+ *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
+ *                           resident blocks (default 33000: four per CU; 0: registers decide)
+ *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,
+ *                           1024-key tiles) or 1 (512-key tiles)
+ *   "contains_emit2_nt"     partitioned contains emit2 shape: 1536 (default: 1024 threads, 12K-pair
+ *                           tiles), 1024 (8K-pair tiles), 1792 (14K), 512 (512 threads, 4K)
+ *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather) */
 int rbx_tune(const char *key, int value);
 #ifdef __cplusplus
 }
