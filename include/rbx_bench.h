@@ -41,7 +41,9 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *   "contains_partition_flags"  diagnostics of that pipeline: 0 (default), 4, 8, 12 (wrong
  *                           answers), 16 (exact: one atomicOr per clear bit, no miss records)
  *   "add_partition"         region-partitioned add: 0 never, 1 always, 2 auto (default:
- *                           bitmap >= 8 MiB, >= 1M keys)
+ *                           bitmap >= 8 MiB and >= max(2^17, bits / 2^12) keys)
+ *   "add_records"           how the partitioned add reports new keys: 0 owner bits, 1 non-owner
+ *                           counters, 3 owner records, 2 (default) chosen from the sampled fill
  *   "add_partition_diag"    0 (default) or 4 (diagnostics)
  *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,
  *                           2 auto (default: the call's bitmaps exceed 64 MiB)
