@@ -8,7 +8,7 @@
 // CAS into a first-setter table, lookups, atomicOr).  Here every (bit, key) pair is routed
 // through two streaming radix passes to its 2^16-bit region, and one workgroup per region resolves
 // the first setters in LDS:
-//   A  k_ba_stage1  : hash, all k pairs per key -> <= 256 level-1 buckets (kBkSub sub-partitions each)
+//   A  k_ba_stage1  : hash, all k pairs per key -> <= 256 level-1 buckets (kBaSub sub-partitions each)
 //   B  k_ba_rebucket: level 1 -> regions (idx >> 16), fan-out <= 256
 //   C  k_ba_region  : region bitmap + met-once / met-again bitsets + a collision table in LDS;
 //                     owners set their bits; the bitmap is written back
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
     __shared__ uint8_t s_bkt[TILE * KMAX];
     __shared__ uint32_t s_cnt[256], s_start[256], s_pos[256], s_gb[256];
     const uint64_t ntiles = (nchunk + TILE - 1) / TILE;
-    const uint32_t sub = blockIdx.x % kBkSub;
+    const uint32_t sub = blockIdx.x % kBaSub;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t maxidx = 0;
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
         if (threadIdx.x < 64) bk_scan256(s_cnt, ncoarse, s_start, s_pos);
         else if (threadIdx.x >= 256 && threadIdx.x - 256 < ncoarse) {
             const uint32_t b = threadIdx.x - 256;
-            if (s_cnt[b]) gb = atomicAdd(&cnt1[b * kBkSub + sub], s_cnt[b]);
+            if (s_cnt[b]) gb = atomicAdd(&cnt1[b * kBaSub + sub], s_cnt[b]);
         }
         __syncthreads();
 #pragma unroll
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
         for (uint32_t i = threadIdx.x; i < total; i += NT) {
             const uint32_t b = s_bkt[i];
             const uint64_t gp = (uint64_t)s_gb[b] + (i - s_start[b]);
-            if (gp < cap1) ba_run_store(s_img[i], p1 + (uint64_t)(b * kBkSub + sub) * cap1 + gp);
+            if (gp < cap1) ba_run_store(s_img[i], p1 + (uint64_t)(b * kBaSub + sub) * cap1 + gp);
             else *overflow = 1u;
         }
         __syncthreads();  // LDS reuse
@@ -542,7 +542,7 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)), dim3(kBaS1Threads), 0, st,
                        a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1, a.overflow);
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
-    hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBkSub, it1, a.s3,
+    hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub, it1, a.s3,
                        a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
     hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(kBaRegionThreads), 0, st, a.p3,
                        a.cnt3, a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,

@@ -538,14 +538,14 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         uint64_t cap = (uint64_t)(pairs * frac * slack) + add;
         return (cap + round - 1) / round * round;
     };
-    const uint64_t cap1 = cap_of(s1, 1.15 / kBkSub, 8192, 8192);
+    const uint64_t cap1 = cap_of(s1, 1.15 / kBaSub, 8192, 8192);
     const uint64_t cap3 = std::min<uint64_t>(kBaMaxRegionPairs, cap_of(s3, 1.3, 256, 64));
-    RBX_TRY(c->pa_p1.reserve((uint64_t)ncoarse * kBkSub * cap1 * 8));
+    RBX_TRY(c->pa_p1.reserve((uint64_t)ncoarse * kBaSub * cap1 * 8));
     RBX_TRY(c->pa_p2.reserve((uint64_t)nregions * cap3 * 8));
     const uint32_t nranges = (uint32_t)((chunk + (1ULL << kBaKeyRangeBits) - 1) >> kBaKeyRangeBits);
     const uint64_t cap_rec = (uint64_t)k << kBaKeyRangeBits;  // a range's owner records <= 2^20 keys x k
     RBX_TRY(c->pa_recs.reserve((uint64_t)nranges * cap_rec * 4));
-    const uint64_t ncnt = (uint64_t)ncoarse * kBkSub + nregions + nranges + 2;
+    const uint64_t ncnt = (uint64_t)ncoarse * kBaSub + nregions + nranges + 2;
     RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
     const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);  // whole ranges (the records kernel's images)
     RBX_TRY(c->pa_bits.reserve(nbw * 4));
@@ -572,7 +572,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.p1 = c->pa_p1.as<unsigned long long>();
         a.p3 = c->pa_p2.as<unsigned long long>();
         a.cnt1 = c->pa_cnt.as<uint32_t>();
-        a.cnt3 = a.cnt1 + (uint64_t)ncoarse * kBkSub;
+        a.cnt3 = a.cnt1 + (uint64_t)ncoarse * kBaSub;
         a.rec_cnt = a.cnt3 + nregions;
         a.overflow = a.rec_cnt + nranges;
         a.mode = a.overflow + 1;

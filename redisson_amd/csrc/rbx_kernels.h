@@ -53,6 +53,10 @@ struct AddChunkArgs {
 // partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
 constexpr int kBkRegionBits = 19;  // 2^19 bits = 64 KiB bitmap region = one LDS image
 constexpr uint32_t kBkSub = 16;    // sub-partitions (own counters) per coarse bucket
+#ifndef RBX_BA_SUB
+#define RBX_BA_SUB 8
+#endif
+constexpr uint32_t kBaSub = RBX_BA_SUB;  // the partitioned add's stage-1 sub-partitions per level-1 bucket
 constexpr int kBkMissRangeBits = 19;  // probe misses are bucketed by 2^19-key range (64 KiB LDS bitmap)
 struct PcArgs {
     KeysDev keys;
