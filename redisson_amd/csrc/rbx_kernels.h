@@ -52,7 +52,10 @@ struct AddChunkArgs {
 
 // partitioned contains (contains_partitioned.hip): one chunk of keys against one filter
 constexpr int kBkRegionBits = 19;  // 2^19 bits = 64 KiB bitmap region = one LDS image
-constexpr uint32_t kBkSub = 16;    // sub-partitions (own counters) per coarse bucket
+#ifndef RBX_BK_SUB
+#define RBX_BK_SUB 16
+#endif
+constexpr uint32_t kBkSub = RBX_BK_SUB;  // sub-partitions (own counters) per coarse bucket
 #ifndef RBX_BA_SUB
 #define RBX_BA_SUB 8
 #endif
