@@ -56,7 +56,8 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *                           1024-key tiles) or 1 (512-key tiles)
  *   "contains_emit2_nt"     partitioned contains emit2 shape: 1536 (default: 1024 threads, 12K-pair
  *                           tiles), 1024 (8K-pair tiles), 1792 (14K), 512 (512 threads, 4K)
- *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather) */
+ *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather)
+ *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048) */
 int rbx_tune(const char *key, int value);
 #ifdef __cplusplus
 }

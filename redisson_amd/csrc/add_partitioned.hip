@@ -533,6 +533,10 @@ __global__ __launch_bounds__(256) void k_ba_final(const uint32_t *__restrict__ n
 }
 
 // launcher ---------------------------------------------------------------------------------
+// EXPERIMENTS (rbx_tune "add_region_grid"): k_ba_region blocks; each walks regions r, r + grid, ...
+static uint32_t g_region_grid = 2048;
+void set_add_region_grid(int v) { g_region_grid = (uint32_t)v; }
+
 template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
     constexpr int TILE = kBaS1Threads * ba_per<KMAX>();
@@ -544,7 +548,7 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
     hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub, it1, a.s3,
                        a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
-    hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(kBaRegionThreads), 0, st, a.p3,
+    hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, g_region_grid)), dim3(kBaRegionThreads), 0, st, a.p3,
                        a.cnt3, a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
                        a.nranges, a.overflow, a.mode, a.diag);
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,

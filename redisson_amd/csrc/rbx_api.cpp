@@ -2669,6 +2669,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_stage1_per(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "add_region_grid")) {
+        if (value < 256 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_grid in [256, 65536]");
+        set_add_region_grid(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "contains_emit2_nt")) {
         if (value != 512 && value != 1024 && value != 1536 && value != 1792)
             return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024, 1536, 1792}");

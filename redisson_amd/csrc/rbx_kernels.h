@@ -95,6 +95,7 @@ inline unsigned grid_for_pc(uint64_t n) {
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
 void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 void set_contains_stage1_per(int v);  // 1 or 2 (default)
+void set_add_region_grid(int v);  // 256..65536 (default 2048)
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 // Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB
