@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- Bloom contains throughput on MI355X (BASELINE.json metric, config C2), with the
-C1 / C3 / C4 legs of the same metric family carried in the same JSON line.
+C1 / C3 / C4 / C5 legs of the same metric family carried in the same JSON line.
 
 Step = one RBloomFilter.contains(Collection) pass (M/RedissonBloomFilter.java:153-186) over a
 batch of 100M synthetic 32-byte keys (50% previously added) against ONE 2^32-bit filter with
 k = 7, keys resident in HBM when the timed region starts.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4|c5] [--legs c1,c3,c4|none]
+  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4|c5] [--legs c1,c3,c4,c5|none]
 
 Multi-GPU: one rank per GPU.  The driver launches N > 1 through torch.distributed.run; when
 WORLD_SIZE is unset and --gpus N > 1, bench.py launches those N ranks itself (a child
@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
-    p.add_argument("--legs", default="c1,c3,c4", help="legs carried in the C2 line: comma list of c1,c3,c4 or 'none'")
+    p.add_argument("--legs", default="c1,c3,c4,c5",
+                   help="legs carried in the C2 line: comma list of c1,c3,c4,c5 or 'none'")
     p.add_argument("--leg-steps", type=int, default=10)
     p.add_argument("--keys", type=int, default=100_000_000, help="keys (C2/C3) or elements (C4) per step per GPU")
     p.add_argument("--tenants", type=int, default=100_000, help="C3 tenant count (whole node)")
@@ -707,7 +708,7 @@ def run_c3(args, world, rank, local, steps, warmup):
 # ------------------------------------------------------------------------------------------
 # C5: ordered 90/10 contains/add stream, Zipf(1.0) tenants over the C3 set, 64-byte keys
 # ------------------------------------------------------------------------------------------
-def run_c5(args, world, rank, local):
+def run_c5(args, world, rank, local, steps, warmup):
     import ctypes as C
 
     import numpy as np
@@ -753,14 +754,14 @@ def run_c5(args, world, rank, local):
         assert L.lib().rbx_bloom_stream_dev(client.ctx, arr, nt, kf.data_ptr(), op.data_ptr(), C.byref(dk), None,
                                              counts.data_ptr(), sptr) == 0
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     barrier(world)
     with Timer(stream) as t:
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
-    ms = t.ms / args.steps
+    ms = t.ms / steps
     step_s = max_over_ranks(world, ms / 1e3)
     value = sum_over_ranks(world, n) / step_s
     top = int(torch.bincount(kf.long(), minlength=nt).max().item())
@@ -774,7 +775,7 @@ def run_c5(args, world, rank, local):
     algo = n * (64 + 10 * 8)
     res = {
         "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
-        "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": value, "unit": "ops/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"C5 ordered stream of {n} single-key commands ({args.add_fraction:.0%} add) over "
@@ -795,6 +796,8 @@ def run_c5(args, world, rank, local):
     for h in handles:
         h.close()
     client.shutdown()
+    del keys, kf, op
+    torch.cuda.empty_cache()
     return res
 
 
@@ -952,7 +955,7 @@ def main():
         ls, lw = min(args.steps, args.leg_steps), min(args.warmup, 2)
         res["legs"] = {}
         for leg in legs:
-            if leg not in ("c1", "c3", "c4"):
+            if leg not in ("c1", "c3", "c4", "c5"):
                 raise SystemExit(f"unknown leg {leg}")
         for leg in legs:
             log(f"[bench] rank {rank} leg {leg}")
@@ -963,6 +966,8 @@ def main():
                     res["legs"]["c1"] = run_c1(args, world, rank, local)
                 elif leg == "c3":
                     res["legs"]["c3"] = run_c3(args, world, rank, local, ls, lw)
+                elif leg == "c5":
+                    res["legs"]["c5"] = run_c5(args, world, rank, local, ls, lw)
                 else:
                     res["legs"]["c4"] = run_c4(args, world, rank, local, ls, lw)
             except Exception as e:  # noqa: BLE001
@@ -975,7 +980,7 @@ def main():
     elif args.workload == "c4":
         res = run_c4(args, world, rank, local, args.steps, args.warmup)
     elif args.workload == "c5":
-        res = run_c5(args, world, rank, local)
+        res = run_c5(args, world, rank, local, args.steps, args.warmup)
     else:
         res = run_c3(args, world, rank, local, args.steps, args.warmup)
     if rank == 0:

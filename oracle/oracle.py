@@ -62,6 +62,8 @@ def _load():
                                               C.c_int]),
         "orc_bloom_add_mt": (C.c_int64, [u8p, u64p, u8p, u64p, C.c_uint64, C.c_int, C.c_int64, u8p, C.c_int]),
         "orc_hash128_batch": (None, [u8p, u64p, C.c_uint64, u64p]),
+        "orc_bloom_stream": (None, [C.POINTER(u8p), u64p, i64p, C.POINTER(C.c_int32), C.POINTER(C.c_uint32), u8p,
+                                    u8p, u64p, C.c_uint64, C.c_uint64, u8p, u64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -211,6 +213,30 @@ class OracleBloom:
     def redis_string(self) -> bytes:
         """What `GET name` returns."""
         return self.bitmap[: self.redis_len].tobytes()
+
+
+def bloom_stream(filters: list, kf: np.ndarray, op: np.ndarray, buf: np.ndarray, offs: np.ndarray | None = None,
+                 stride: int = 0):
+    """An ordered stream of single-key add(T)/contains(T) commands (orc_bloom_stream): command i
+    runs on filters[kf[i]] (OracleBloom objects, updated in place) in index order.  Keys: an arena
+    (buf, offs) or fixed-stride bytes (offs None).  Returns (replies u8[n], [present, added])."""
+    n = int(kf.size)
+    kf = np.ascontiguousarray(kf, dtype=np.uint32)
+    op = np.ascontiguousarray(op, dtype=np.uint8)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    bms = (u8p * len(filters))(*[_p(f.bitmap) for f in filters])
+    lens = np.array([f.redis_len for f in filters], dtype=np.uint64)
+    sizes = np.array([f.size for f in filters], dtype=np.int64)
+    ks = np.array([f.k for f in filters], dtype=np.int32)
+    assert int(ks.max()) <= 64 and (n == 0 or int(kf.max()) < len(filters))
+    out = np.zeros(max(n, 1), np.uint8)
+    cnt = np.zeros(2, np.uint64)
+    lib().orc_bloom_stream(bms, _p(lens, u64p), _p(sizes, i64p), ks.ctypes.data_as(C.POINTER(C.c_int32)),
+                           kf.ctypes.data_as(C.POINTER(C.c_uint32)), _p(op), _p(buf),
+                           _p(offs, u64p) if offs is not None else None, int(stride), n, _p(out), _p(cnt, u64p))
+    for f, ln in zip(filters, lens):
+        f.redis_len = int(ln)
+    return out[:n], [int(cnt[0]), int(cnt[1])]
 
 
 def java_math_round(x: float) -> int:

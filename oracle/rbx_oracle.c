@@ -315,6 +315,45 @@ int64_t orc_bloom_contains(const uint8_t *bitmap, uint64_t redis_len, const uint
     return (int64_t)n - missed;
 }
 
+/* An ordered stream of single-key commands (BASELINE config 5): command i is add(T) (op[i] != 0)
+ * or contains(T) (op[i] == 0) on filter kf[i], executed one after another.  add(T) is
+ * add(Arrays.asList(T)) > 0 (M/RedissonBloomFilter.java:99-102) and contains(T) is
+ * contains(Arrays.asList(T)) > 0 (:198-201), i.e. one k-command batch per key.  Filter f is
+ * bitmaps[f] / redis_lens[f] with sizes[f] bits and ks[f] hash iterations (k <= 64).  Keys: an
+ * arena (offsets, n+1 entries) or, when offsets is NULL, fixed stride bytes.  out[i] = the
+ * boolean reply; out_counts = {present contains, new adds}. */
+void orc_bloom_stream(uint8_t *const *bitmaps, uint64_t *redis_lens, const int64_t *sizes, const int32_t *ks,
+                      const uint32_t *kf, const uint8_t *op, const uint8_t *bytes, const uint64_t *offsets,
+                      uint64_t stride, uint64_t n, uint8_t *out, uint64_t *out_counts) {
+    int64_t idx[64];
+    uint64_t present = 0, added = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t f = kf[i];
+        const uint64_t a = offsets ? offsets[i] : i * stride;
+        const uint64_t len = offsets ? offsets[i + 1] - offsets[i] : stride;
+        uint64_t h[2];
+        orc_redisson_hash128(bytes + a, (size_t)len, h);
+        const int k = ks[f];
+        orc_bloom_indexes(h[0], h[1], k, sizes[f], idx);
+        int zeros = 0;
+        if (op[i]) {
+            for (int j = 0; j < k; j++)
+                if (!setbit(bitmaps[f], &redis_lens[f], (uint64_t)idx[j])) zeros++;
+            out[i] = zeros > 0;
+            added += zeros > 0;
+        } else {
+            for (int j = 0; j < k; j++)
+                if (!getbit(bitmaps[f], redis_lens[f], (uint64_t)idx[j])) zeros++;
+            out[i] = zeros == 0;
+            present += zeros == 0;
+        }
+    }
+    if (out_counts) {
+        out_counts[0] = present;
+        out_counts[1] = added;
+    }
+}
+
 /* BITCOUNT over the whole string [redis-7.2 bitops.c]. */
 uint64_t orc_bitcount(const uint8_t *bitmap, uint64_t redis_len) {
     uint64_t c = 0;

@@ -37,7 +37,20 @@ SerialExecutor::~SerialExecutor() {
         stop_ = true;
     }
     cv_.notify_all();
-    if (th_.joinable()) th_.join();
+    if (th_.joinable() && th_.get_id() != std::this_thread::get_id()) th_.join();
+}
+
+bool SerialExecutor::on_executor_thread() const {
+    return started_ && th_.get_id() == std::this_thread::get_id();
+}
+
+void SerialExecutor::release_from_inside(SerialExecutor *e) {
+    {
+        std::lock_guard<std::mutex> g(e->mu_);
+        e->stop_ = true;
+        e->self_delete_ = true;
+    }
+    e->th_.detach();  // loop() deletes the executor once the queue is empty
 }
 
 std::shared_ptr<Future> SerialExecutor::submit(std::function<int()> fn, AsyncCallback cb, void *user) {
@@ -46,14 +59,17 @@ std::shared_ptr<Future> SerialExecutor::submit(std::function<int()> fn, AsyncCal
     f->user = user;
     {
         std::lock_guard<std::mutex> g(mu_);
+        if (stop_) return nullptr;
         if (!started_) {
             th_ = std::thread([this] { loop(); });
             started_ = true;
         }
         q_.push_back(Task{std::move(fn), f});
         submitted_++;
+        // notified under the lock: once it is released the task may run, and a completion
+        // callback may release the executor from inside (release_from_inside), which then frees it
+        cv_.notify_all();
     }
-    cv_.notify_all();
     return f;
 }
 
@@ -69,7 +85,13 @@ void SerialExecutor::loop() {
         {
             std::unique_lock<std::mutex> g(mu_);
             cv_.wait(g, [&] { return stop_ || !q_.empty(); });
-            if (q_.empty()) return;  // stop requested and nothing left
+            if (q_.empty()) {  // stop requested and nothing left
+                if (self_delete_) {
+                    g.unlock();
+                    delete this;  // detached by release_from_inside(); nobody else owns it
+                }
+                return;
+            }
             t = std::move(q_.front());
             q_.pop_front();
         }

@@ -42,8 +42,15 @@ public:
     SerialExecutor &operator=(const SerialExecutor &) = delete;
     ~SerialExecutor();  // runs what is queued, then joins the thread
 
+    // nullptr once the executor is stopping (the caller reports the context as shut down)
     std::shared_ptr<Future> submit(std::function<int()> fn, AsyncCallback cb, void *user);
     void drain();  // returns once everything submitted so far has completed
+    // true on the executor's own thread (a completion callback)
+    bool on_executor_thread() const;
+    // Stop from the executor's own thread: later submits are refused, what is queued still runs,
+    // and the executor frees itself when its thread leaves the loop (it cannot join itself).
+    // The caller gives up ownership.
+    static void release_from_inside(SerialExecutor *e);
 
 private:
     struct Task {
@@ -57,6 +64,7 @@ private:
     std::deque<Task> q_;
     bool stop_ = false;
     bool started_ = false;
+    bool self_delete_ = false;
     uint64_t submitted_ = 0, completed_ = 0;
     std::condition_variable idle_;
     std::thread th_;

@@ -180,6 +180,9 @@ struct rbx_ctx {
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
+    // all-zero words standing in for a missing bitmap in multi-tenant contains (GETBIT on a
+    // missing key reads 0; the key is not created), grown on demand, never written by a kernel
+    DevBuf zero_bm;
     DevBuf hll_pack;                                // contiguous registers for the RCCL merge
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
@@ -188,6 +191,7 @@ struct rbx_ctx {
     // the handle list filt_table was built from (fast path for repeated multi-tenant calls)
     std::vector<std::pair<const rbx_bloom *, uint64_t>> filt_keys;
     uint64_t filt_key_generation = ~0ULL, filt_bytes = 0;
+    bool filt_create = false;
     uint32_t filt_kmax = 1;
 
     std::shared_ptr<SlabPool> slab = std::make_shared<SlabPool>();
@@ -213,7 +217,9 @@ struct rbx_ctx {
     hipStream_t scratch_stream = nullptr;
 
     // the asynchronous entry points' serial executor (host_exec.h): its thread starts with the
-    // first *_async call
+    // first *_async call.  exec_mu guards the pointer: rbx_shutdown takes the executor out under
+    // it, so a submit either lands before (and runs) or is refused.
+    std::mutex exec_mu;
     std::unique_ptr<SerialExecutor> exec = std::make_unique<SerialExecutor>();
 };
 
@@ -764,8 +770,20 @@ int rbx_init(int device, rbx_ctx **out) {
 // closed (closing a handle after shutdown is safe, every other call on it fails).
 int rbx_shutdown(rbx_ctx *c) {
     if (!c) return RBX_OK;
-    // queued asynchronous calls run to completion first (they take the context lock themselves)
-    if (c->exec) c->exec.reset();
+    // Queued asynchronous calls run to completion first (they take the context lock themselves):
+    // the executor is taken out under exec_mu (later submits are refused), then destroyed, which
+    // runs its queue and joins its thread.  From a completion callback (the executor's own
+    // thread) it cannot join itself: it is detached, runs what is queued -- those calls fail with
+    // RBX_E_ILLEGAL_STATE once the context is shut -- and frees itself.
+    std::unique_ptr<SerialExecutor> ex;
+    {
+        std::lock_guard<std::mutex> g(c->exec_mu);
+        ex = std::move(c->exec);
+    }
+    if (ex) {
+        if (ex->on_executor_thread()) SerialExecutor::release_from_inside(ex.release());
+        else ex.reset();
+    }
     {
         std::lock_guard<std::recursive_mutex> g(c->ks.mu);
         if (c->shut) return fail(RBX_E_ILLEGAL_STATE, "the context has already been shut down");
@@ -783,7 +801,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->counters, &c->filt_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
-                          &c->st_prefilter, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
+                          &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1]}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
@@ -1184,10 +1202,13 @@ static int bloom_open(rbx_ctx *c, const std::string &name, rbx_bloom **out) {
     BloomConfig cfg;
     RBX_TRY(ks_get_config(c->ks, name, &cfg));
     RBX_TRY(check_offsets(cfg.size));
+    // Opening a handle is RedissonBloomFilter's constructor + readConfig: it creates no bitmap
+    // key (the first SETBIT does), so EXISTS / DEL / sizeInMemory see what the reference sees.
     std::shared_ptr<Bitmap> bm;
-    RBX_TRY(bitmap_for(c, name, size_bits(cfg.size), true, c->stream, &bm));
+    RBX_TRY(bitmap_for(c, name, size_bits(cfg.size), false, c->stream, &bm));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    *out = new rbx_bloom{c, name, cfg.size, cfg.k, bm, c->ks.generation, g_handle_serial++};
+    // gen 0 (never current: generations start at 1) makes the first call bind a missing bitmap
+    *out = new rbx_bloom{c, name, cfg.size, cfg.k, bm, bm ? c->ks.generation : 0, g_handle_serial++};
     c->refs.fetch_add(1);
     return RBX_OK;
 }
@@ -1236,7 +1257,8 @@ static int bloom_bind(rbx_ctx *c, rbx_bloom *b, bool create, hipStream_t st, boo
     RBX_TRY(bitmap_for(c, b->name, size_bits(b->size), create, st, &bm));
     if (!bm) {
         *absent = true;
-        return RBX_OK;
+        b->bm.reset();  // a deleted bitmap's memory is not held by the handle
+        return RBX_OK;  // (gen stays stale: the next call binds again)
     }
     b->bm = bm;
     b->gen = c->ks.generation;
@@ -1287,12 +1309,14 @@ int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t 
 static int g_multi_slots = 2;
 constexpr uint64_t kSlotsMinBytes = 64ULL << 20;
 
+// create: a missing bitmap is created (add, stream); otherwise (contains) it reads as all zero
+// through c->zero_bm and stays missing.
 static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, uint32_t *kmax, hipStream_t st,
-                          uint64_t *distinct_bytes = nullptr) {
+                          bool create, uint64_t *distinct_bytes = nullptr) {
     c->ks.sweep();
     // same handles as the previous call and no keyspace change since: filt_table is current
     // (100k tenants: ~5 ms of host work per call otherwise, more than the kernel takes)
-    if (c->filt_key_generation == c->ks.generation && c->filt_keys.size() == nseg) {
+    if (c->filt_key_generation == c->ks.generation && c->filt_keys.size() == nseg && c->filt_create == create) {
         bool same = true;
         for (uint32_t s = 0; s < nseg && same; ++s)
             same = filters[s] && c->filt_keys[s].first == filters[s] && c->filt_keys[s].second == filters[s]->serial;
@@ -1306,14 +1330,22 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
     std::unordered_map<const Bitmap *, uint32_t> fid;
     uint32_t km = 1;
     uint64_t bytes = 0;
+    std::vector<uint32_t> absent_segs;
+    uint64_t zero_bytes = 0;
     for (uint32_t s = 0; s < nseg; ++s) {
         rbx_bloom *b = filters[s];
         if (!b) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL filter handle");
-        if (b->gen != c->ks.generation) {  // (a missing bitmap is created: the kernels need one)
+        if (b->gen != c->ks.generation) {
             bool absent;
-            RBX_TRY(bloom_bind(c, b, true, st, &absent));
+            RBX_TRY(bloom_bind(c, b, create, st, &absent));
         }
         RBX_TRY(check_offsets(b->size));
+        km = std::max(km, b->k);
+        if (!b->bm) {  // contains on a missing key: every GETBIT reads 0
+            absent_segs.push_back(s);
+            zero_bytes = std::max<uint64_t>(zero_bytes, (size_bits(b->size) + 7) / 8);
+            continue;
+        }
         auto it = fid.find(b->bm.get());
         uint32_t id = it == fid.end() ? (uint32_t)fid.size() : it->second;
         if (it == fid.end()) {
@@ -1322,7 +1354,25 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
         }
         if (id >= (1u << 24)) return fail(RBX_E_ILLEGAL_ARGUMENT, "more than 2^24 distinct filters in one call");
         v[s] = desc_of(*b->bm, size_bits(b->size), b->k, id);
-        km = std::max(km, b->k);
+    }
+    if (!absent_segs.empty()) {
+        // zero words for the largest missing bitmap + a zero Redis-length word (never written)
+        const uint64_t need = ((zero_bytes + 255) & ~255ULL) + 256;
+        if (c->zero_bm.cap < need) {
+            RBX_TRY(c->zero_bm.reserve(need));
+            HIP_TRY(hipMemsetAsync(c->zero_bm.p, 0, c->zero_bm.cap, st));
+        }
+        const uint32_t zid = (uint32_t)fid.size();
+        for (uint32_t s : absent_segs) {
+            rbx_bloom *b = filters[s];
+            FilterDesc f{};
+            f.bm = c->zero_bm.as<uint32_t>();
+            f.redis_len = (unsigned long long *)((uint8_t *)c->zero_bm.p + need - 256);
+            f.mp = make_mod_params(size_bits(b->size));
+            f.k = b->k;
+            f.fid = zid;
+            v[s] = f;
+        }
     }
     *kmax = km;
     bool same = c->filt_generation == c->ks.generation && c->filt_cache.size() == v.size() &&
@@ -1337,6 +1387,7 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
     c->filt_keys.resize(nseg);
     for (uint32_t s = 0; s < nseg; ++s) c->filt_keys[s] = {filters[s], filters[s]->serial};
     c->filt_key_generation = c->ks.generation;
+    c->filt_create = create;
     c->filt_kmax = km;
     c->filt_bytes = bytes;
     if (distinct_bytes) *distinct_bytes = bytes;
@@ -1354,7 +1405,7 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
     uint64_t bytes = 0;
-    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, &bytes));
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, false, &bytes));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
     RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
@@ -1376,7 +1427,7 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     ScratchOrder so_(c, pick_stream(c, stream));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
-    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st));
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, true));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
     RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
@@ -1387,6 +1438,8 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
 }
 
 // Ordered mixed stream (C5): see rbx.h.  Chunks of <= 2^26 pairs run probe -> contains -> commit.
+// rbx_tune("stream_chunk", n) caps a chunk at n commands (tests: many chunks on small streams).
+static uint64_t g_stream_chunk = 0;
 int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
                          const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
                          unsigned long long *d_counts, void *stream) {
@@ -1398,12 +1451,13 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     ScratchOrder so_(c, pick_stream(c, stream));
     hipStream_t st = pick_stream(c, stream);
     uint32_t kmax;
-    RBX_TRY(upload_filters(c, filters, nfilters, &kmax, st));
+    RBX_TRY(upload_filters(c, filters, nfilters, &kmax, st, true));
     if (kmax > 32) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream batches support k <= 32");
     if (d_keys->n == 0) return RBX_OK;
     KeysDev keys = keys_dev(d_keys);
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, (1ULL << 26) / k));
+    if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_adds.reserve(chunk * 4));
     constexpr uint64_t kPrefilterWords = 1ULL << (25 - 5);  // bloom_kernels.hip kPrefilterBits
@@ -2313,11 +2367,24 @@ int rbx_hll_allreduce_max(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n) {
 // key bytes and output buffers are read / written when the call runs (valid until completion).
 static int submit_async(rbx_ctx *c, std::function<int()> fn, rbx_callback cb, void *user, rbx_future **out) {
     if (!c || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
-    {
-        std::lock_guard<std::recursive_mutex> g(c->ks.mu);
-        if (c->shut || !c->exec) return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
+    // exec_mu is held through the submit, so rbx_shutdown cannot free the executor under it; the
+    // queued call holds a context reference until it has run (the context outlives a shutdown
+    // issued from a completion callback while calls are still queued).
+    std::lock_guard<std::mutex> g(c->exec_mu);
+    if (!c->exec) return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
+    c->refs.fetch_add(1);
+    auto f = c->exec->submit(
+        [c, fn = std::move(fn)]() {
+            const int rc = fn();
+            ctx_release(c);
+            return rc;
+        },
+        cb, user);
+    if (!f) {
+        ctx_release(c);
+        return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
     }
-    *out = new rbx_future{c->exec->submit(std::move(fn), cb, user)};
+    *out = new rbx_future{std::move(f)};
     return RBX_OK;
 }
 
@@ -2647,6 +2714,11 @@ int rbx_tune(const char *key, int value) {
         if (value != 22 && value != 24 && value != 32 && value != 34 && value != 42 && value != 44)
             return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qshape in {22, 24, 32, 34, 42, 44}");
         set_contains_qshape(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_chunk")) {
+        if (value < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_chunk >= 0 (0: 2^26 / k commands)");
+        g_stream_chunk = (uint64_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_contains_slots")) {

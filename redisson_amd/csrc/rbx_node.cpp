@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -22,11 +23,25 @@
 
 using namespace rbx;
 
+// A cached Bloom handle, closed when the last holder lets go: the cache holds one reference and
+// every in-flight batch holds its own, so a handle evicted (DEL) or replaced (config re-created)
+// while another thread still runs a batch on it is closed when that batch ends.
+struct NodeHandle {
+    rbx_bloom *h = nullptr;
+    ~NodeHandle() {
+        if (h) rbx_bloom_close(h);
+    }
+};
+using HandleRef = std::shared_ptr<NodeHandle>;
+
+// Above this many cached handles the cache is emptied (handles are re-opened on demand): a
+// long-lived node with tenant churn does not keep one handle per name it ever served.
+constexpr size_t kMaxCachedHandles = 1u << 20;
+
 struct rbx_node {
     std::vector<rbx_ctx *> ctx;
-    std::mutex mu;                                            // the handle cache
-    std::map<std::pair<int, std::string>, rbx_bloom *> blooms;  // open handles per (GPU, name)
-    std::vector<rbx_bloom *> retired;                         // replaced handles, closed at shutdown
+    std::mutex mu;                                           // the handle cache
+    std::map<std::pair<int, std::string>, HandleRef> blooms;  // open handles per (GPU, name)
 };
 
 static std::atomic<uint64_t> g_tmp_serial{1};
@@ -96,8 +111,7 @@ int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
 
 int rbx_node_shutdown(rbx_node *nd) {
     if (!nd) return RBX_OK;
-    for (auto &kv : nd->blooms) rbx_bloom_close(kv.second);
-    for (rbx_bloom *b : nd->retired) rbx_bloom_close(b);
+    nd->blooms.clear();  // closes every cached handle (no batch may run during shutdown)
     int rc = RBX_OK;
     for (rbx_ctx *c : nd->ctx) {
         const int r = rbx_shutdown(c);
@@ -166,6 +180,19 @@ int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) 
         NODE_TRY(check_name(names[i]));
         by[gpu_of(nd, str_of(names[i]))].push_back(names[i]);
     }
+    // the deleted names' cached handles go too (each holds its bitmap until its next call)
+    std::vector<HandleRef> evicted;
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        for (uint32_t i = 0; i < n; ++i) {
+            auto it = nd->blooms.find(std::make_pair(gpu_of(nd, str_of(names[i])), str_of(names[i])));
+            if (it != nd->blooms.end()) {
+                evicted.push_back(std::move(it->second));
+                nd->blooms.erase(it);
+            }
+        }
+    }
+    evicted.clear();  // outside the cache lock: closing takes the context lock
     int total = 0;
     for (size_t g = 0; g < by.size(); ++g) {
         if (by[g].empty()) continue;
@@ -237,23 +264,28 @@ static std::vector<int> gpus_with_work(const std::vector<Part> &parts) {
 
 // the cached handle of (gpu, name); refresh = replace it with a freshly opened one (the config was
 // re-created with other parameters: a new RBloomFilter object would read the new config)
-static int bloom_handle(rbx_node *nd, int g, const std::string &name, bool refresh, rbx_bloom **out) {
-    std::lock_guard<std::mutex> lk(nd->mu);
+static int bloom_handle(rbx_node *nd, int g, const std::string &name, bool refresh, HandleRef *out) {
     auto key = std::make_pair(g, name);
-    auto it = nd->blooms.find(key);
-    if (it != nd->blooms.end() && !refresh) {
-        *out = it->second;
-        return RBX_OK;
+    HandleRef old;  // a replaced handle is closed outside the cache lock (when its users are done)
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        auto it = nd->blooms.find(key);
+        if (it != nd->blooms.end() && !refresh) {
+            *out = it->second;
+            return RBX_OK;
+        }
     }
-    rbx_bloom *b = nullptr;
-    NODE_TRY(rbx_bloom_open_n(nd->ctx[g], name_ref(name), &b));
-    if (it != nd->blooms.end()) {
-        nd->retired.push_back(it->second);  // another thread may still be using it
-        it->second = b;
-    } else {
-        nd->blooms[key] = b;
+    auto ref = std::make_shared<NodeHandle>();
+    NODE_TRY(rbx_bloom_open_n(nd->ctx[g], name_ref(name), &ref->h));
+    std::map<std::pair<int, std::string>, HandleRef> flushed;
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        if (nd->blooms.size() >= kMaxCachedHandles) flushed.swap(nd->blooms);
+        HandleRef &slot = nd->blooms[key];
+        old = std::move(slot);
+        slot = ref;
     }
-    *out = b;
+    *out = ref;
     return RBX_OK;
 }
 
@@ -269,8 +301,12 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
     const int rc = per_gpu(gpus, [&](int g) -> int {
         Part &p = parts[g];
         for (int attempt = 0;; ++attempt) {
+            std::vector<HandleRef> refs(p.segs.size());  // held for the batch
             std::vector<rbx_bloom *> hs(p.segs.size());
-            for (size_t j = 0; j < p.segs.size(); ++j) NODE_TRY(bloom_handle(nd, g, sn[p.segs[j]], attempt > 0, &hs[j]));
+            for (size_t j = 0; j < p.segs.size(); ++j) {
+                NODE_TRY(bloom_handle(nd, g, sn[p.segs[j]], attempt > 0, &refs[j]));
+                hs[j] = refs[j]->h;
+            }
             const auto fn = is_add ? rbx_bloom_add_multi : rbx_bloom_contains_multi;
             const int r = fn(nd->ctx[g], hs.data(), (uint32_t)hs.size(), p.seg.data(), &p.keys,
                              out ? p.out.data() : nullptr, p.cnt.data());

@@ -296,6 +296,91 @@ static void test_executor() {
     }
     CHECK(overlap.load() == 0 && order_errors.load() == 0);
     CHECK(g_cb_calls.load() == 6 * 400 + 1 + 50);
+
+    // rbx_shutdown's pattern: submitters race a teardown that takes the executor out
+    // under the same mutex; every submit either returns a future that completes or is refused
+    {
+        std::mutex emu;
+        std::unique_ptr<SerialExecutor> owner = std::make_unique<SerialExecutor>();
+        std::atomic<long> accepted{0}, refused{0}, ran{0};
+        std::vector<std::shared_ptr<Future>> got[4];
+        std::vector<std::thread> th;
+        for (int t = 0; t < 4; ++t) {
+            th.emplace_back([&, t]() {
+                for (int i = 0; i < 3000; ++i) {
+                    std::lock_guard<std::mutex> g(emu);
+                    if (!owner) {
+                        refused++;
+                        continue;
+                    }
+                    auto f = owner->submit([&]() -> int { ran++; return RBX_OK; }, nullptr, nullptr);
+                    if (f) {
+                        accepted++;
+                        got[t].push_back(f);
+                    } else {
+                        refused++;
+                    }
+                }
+            });
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        std::unique_ptr<SerialExecutor> out;
+        {
+            std::lock_guard<std::mutex> g(emu);
+            out = std::move(owner);
+        }
+        out.reset();  // runs the queue, joins
+        for (auto &x : th) x.join();
+        CHECK(accepted.load() + refused.load() == 4 * 3000);
+        CHECK(ran.load() == accepted.load());
+        for (auto &v : got)
+            for (auto &f : v) CHECK(f->wait(0) && f->rc == RBX_OK);
+    }
+    // shutdown from a completion callback: the executor cannot join its own thread, so it is
+    // released from inside, refuses later submits, still runs what was queued and frees itself
+    {
+        std::mutex emu;
+        SerialExecutor *raw = new SerialExecutor();
+        std::unique_ptr<SerialExecutor> owner(raw);
+        struct Ctx {
+            std::mutex *emu;
+            std::unique_ptr<SerialExecutor> *owner;
+            std::atomic<int> released{0};
+        } cx{&emu, &owner};
+        auto cb = [](void *u, int) {
+            auto *x = (Ctx *)u;
+            std::unique_ptr<SerialExecutor> e;
+            {
+                std::lock_guard<std::mutex> g(*x->emu);
+                e = std::move(*x->owner);
+            }
+            if (e) {
+                CHECK(e->on_executor_thread());
+                SerialExecutor::release_from_inside(e.release());
+                x->released++;
+            }
+        };
+        std::atomic<int> after{0};
+        auto f0 = raw->submit([]() -> int { return RBX_OK; }, cb, &cx);
+        std::vector<std::shared_ptr<Future>> queued;
+        for (int i = 0; i < 20; ++i) {  // through the owner, as rbx_api.cpp's submit_async does
+            std::lock_guard<std::mutex> g(emu);
+            queued.push_back(owner ? owner->submit([&]() -> int { after++; return RBX_OK; }, nullptr, nullptr)
+                                   : nullptr);
+        }
+        CHECK(f0->wait(-1));
+        for (auto &f : queued)
+            if (f) CHECK(f->wait(-1));
+        CHECK(cx.released.load() == 1);
+        {
+            std::lock_guard<std::mutex> g(emu);
+            CHECK(!owner);
+        }
+        int accepted = 0;
+        for (auto &f : queued) accepted += f != nullptr;
+        CHECK(after.load() == accepted);
+        std::this_thread::sleep_for(std::chrono::milliseconds(200));  // the detached thread frees it
+    }
 }
 
 int main() {

@@ -88,3 +88,90 @@ def test_async_bloom_add_then_contains_in_order(client, fresh):
     assert c1.value == cr and np.array_equal(new, nr)
     assert c2.value == 50_000 and pres.all()
     f.delete()
+
+
+def _wait_all(futs):
+    """(accepted rc list) -- every accepted future completes; none hangs."""
+    out = []
+    for fp in futs:
+        rc = C.c_int(-99)
+        assert L.lib().rbx_future_wait(fp, 60_000, C.byref(rc)) == 0, "an accepted call never completed"
+        out.append(rc.value)
+        L.lib().rbx_future_free(fp)
+    return out
+
+
+def test_async_submit_races_shutdown():
+    """*_async submits on several threads while another thread shuts the context down.
+    Every submit is either accepted (and its future completes: OK, or ILLEGAL_STATE when it ran after
+    the shutdown) or refused with RBX_E_ILLEGAL_STATE; nothing hangs or touches a freed executor."""
+    import threading
+
+    from redisson_amd import RedissonClient
+
+    c = RedissonClient(0)
+    ctx = c.ctx
+    c.getHyperLogLog("race").add(b"x")
+    # an open handle keeps the context object alive past rbx_shutdown (calls then fail cleanly)
+    hold = C.c_void_p()
+    assert L.lib().rbx_hll_open(ctx, b"race", 1, C.byref(hold)) == 0
+    accepted, refused, lock = [], [], threading.Lock()
+    keys = Arena([b"a", b"b", b"c"])
+
+    def submitter():
+        for _ in range(300):
+            fp = C.c_void_p()
+            changed = C.c_int()
+            rc = L.lib().rbx_hll_add_async(ctx, b"race", keys.ptr(), C.byref(changed), None, None, C.byref(fp))
+            with lock:
+                (accepted if rc == 0 else refused).append(fp if rc == 0 else rc)
+
+    th = [threading.Thread(target=submitter) for _ in range(4)]
+    for t in th:
+        t.start()
+    c.shutdown()
+    for t in th:
+        t.join()
+    assert all(r == L.RBX_E_ILLEGAL_STATE for r in refused)
+    rcs = _wait_all(accepted)
+    assert all(r in (0, L.RBX_E_ILLEGAL_STATE) for r in rcs)
+    assert len(accepted) + len(refused) == 1200
+    assert L.lib().rbx_hll_close(hold) == 0
+
+
+def test_shutdown_from_completion_callback():
+    """a completion callback (the executor's own thread) calls rbx_shutdown.  The call
+    returns, the executor is released from inside instead of joining itself, calls queued behind it
+    complete (with RBX_E_ILLEGAL_STATE: the context is shut), and later submits are refused."""
+    from redisson_amd import RedissonClient
+
+    c = RedissonClient(0)
+    ctx = c.ctx
+    hold = C.c_void_p()
+    assert L.lib().rbx_hll_open(ctx, b"cbshut", 1, C.byref(hold)) == 0  # keeps the context object alive
+    state = {}
+    CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+
+    def on_done(user, rc):
+        if user == 1:
+            state["shutdown_rc"] = L.lib().rbx_shutdown(ctx)
+
+    cb = CB(on_done)
+    keys = Arena([b"k"])
+    futs = []
+    for i in range(1, 6):
+        fp = C.c_void_p()
+        changed = C.c_int()
+        assert L.lib().rbx_hll_add_async(ctx, b"cbshut", keys.ptr(), C.byref(changed), C.cast(cb, C.c_void_p),
+                                         C.c_void_p(i), C.byref(fp)) in (0, L.RBX_E_ILLEGAL_STATE)
+        if fp.value:
+            futs.append(fp)
+    rcs = _wait_all(futs)
+    assert rcs[0] == 0 and state["shutdown_rc"] == 0
+    assert all(r in (0, L.RBX_E_ILLEGAL_STATE) for r in rcs[1:])
+    fp = C.c_void_p()
+    changed = C.c_int()
+    assert L.lib().rbx_hll_add_async(ctx, b"cbshut", keys.ptr(), C.byref(changed), None, None,
+                                     C.byref(fp)) == L.RBX_E_ILLEGAL_STATE
+    assert L.lib().rbx_hll_close(hold) == 0
+    c._ctx = C.c_void_p()  # already shut from the callback

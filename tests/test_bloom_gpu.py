@@ -1033,3 +1033,94 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
         assert bitmaps[i] == bitmaps[0], runs[i]
     del keys, flags
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_bitset_vectors_on_gpu(client, fresh, case):
+    """T/RedissonBitSetTest.java:140-186 on the engine: each test's SETBIT sequence replayed as an add()
+    of keys that hit the chosen bits of a raw (64, 1) filter; the exported Redis string has the
+    reference's size() = STRLEN * 8 and cardinality() = BITCOUNT, bits MSB-first."""
+    from bitset_vectors import BITSET_VECTORS, key_for_bit
+
+    bits, size_bits, card = BITSET_VECTORS[case]
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(64, 1)
+    assert f.exportBitmap() == b""  # size() 0 before any SETBIT
+    keys = [key_for_bit(b) for b in bits]
+    c, new = f.addEach(Arena(keys))
+    assert c == len(bits) and new.all()
+    s = f.exportBitmap()
+    assert len(s) * 8 == size_bits and f.bitcount() == card
+    assert [i for i in range(len(s) * 8) if s[i >> 3] & (0x80 >> (i & 7))] == sorted(bits)
+    assert f.contains(Arena([key_for_bit(0)])) == (1 if 0 in bits else 0)
+    ref = O.OracleBloom(64, 1)
+    ref.add(*O.arena(keys))
+    assert s == ref.redis_string()
+    f.delete()
+
+
+def test_c3_full_tenant_count_slot_kernel(client, fresh):
+    """C3 at its real size: 100k tryInit(1e6, 1e-3) tenants (14,377,587 bits each, 179.7 GB of
+    slab-allocated bitmaps imported from slices of a device pool, as bench.py's C3 leg builds them),
+    then one contains_multi batch of 24 16-byte keys per tenant on the default kernel for that size
+    (the per-lane slot kernel, > 64 MiB of bitmaps).  1,000 sampled tenants first get 8 keys each
+    through add_multi (one 100k-filter batch, epoch-tagged first-setter table), mirrored on oracle
+    filters rebuilt from the same pool slices; their per-key contains flags and counts must match."""
+    import ctypes as C
+
+    import torch
+
+    from redisson_amd import _lib as L
+
+    nt, per, nsample = 100_000, 24, 1000
+    rng = np.random.default_rng(0x5EED0003)
+    pool = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    dpool = torch.from_numpy(pool).cuda()
+    names = [f"{fresh}:{t:06d}" for t in range(nt)]
+    offs = np.zeros(nt, np.int64)
+    handles = []
+    try:
+        for t, nm in enumerate(names):
+            f = client.getBloomFilter(nm)
+            assert f.tryInit(1_000_000, 1e-3)
+            nb = (14_377_587 + 7) // 8
+            offs[t] = int(rng.integers(0, (pool.size - nb) // 256)) * 256
+            assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), dpool.data_ptr() + int(offs[t]), nb,
+                                                None) == 0
+            handles.append(BloomHandle(client, nm))
+        assert (handles[0].size, handles[0].k) == (14_377_587, 10)
+        sample = np.sort(rng.choice(nt, size=nsample, replace=False))
+        refs = {}
+        for t in sample:
+            r = O.OracleBloom(14_377_587, 10)
+            nb = (14_377_587 + 7) // 8
+            r.bitmap[:nb] = pool[offs[t]:offs[t] + nb]
+            r.redis_len = nb
+            refs[int(t)] = r
+        # adds: 8 keys into each sampled tenant, one multi-tenant add batch
+        add_keys = rng.integers(0, 256, size=(nsample * 8, 16), dtype=np.uint8)
+        aseg = np.arange(nsample + 1, dtype=np.uint64) * np.uint64(8)
+        acounts, aflags = bloom_add_multi(client, [handles[t] for t in sample], aseg, Arena.fixed(add_keys),
+                                          per_key=True)
+        for s, t in enumerate(sample):
+            c, fl = refs[int(t)].add(*O.fixed_arena(add_keys[8 * s:8 * s + 8]), per_key=True)
+            assert acounts[s] == c and np.array_equal(aflags[8 * s:8 * s + 8], fl)
+        # contains: per keys per tenant, the sampled tenants' first 8 keys are their added ones
+        keys = rng.integers(0, 256, size=(nt * per, 16), dtype=np.uint8)
+        for s, t in enumerate(sample):
+            keys[t * per:t * per + 8] = add_keys[8 * s:8 * s + 8]
+        seg = np.arange(nt + 1, dtype=np.uint64) * np.uint64(per)
+        counts, flags = bloom_contains_multi(client, handles, seg, Arena.fixed(keys), per_key=True)
+        for t in sample:
+            t = int(t)
+            c, fl = refs[t].contains(*O.fixed_arena(keys[t * per:(t + 1) * per]), per_key=True)
+            assert counts[t] == c and np.array_equal(flags[t * per:(t + 1) * per], fl), t
+            assert c >= 8
+        assert int(counts.sum()) == int(flags.sum())
+    finally:
+        for h in handles:
+            h.close()
+        for nm in names:
+            client.getBloomFilter(nm).delete()
+        del dpool
+        torch.cuda.empty_cache()

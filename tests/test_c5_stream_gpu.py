@@ -1,0 +1,103 @@
+"""BASELINE config 5 on the GPU: the ordered mixed contains/add stream with C5's own kernel
+instantiation -- 64-byte fixed keys (KLEN = 64) on tryInit(1e6, 1e-3) tenants (m = 14,377,587,
+k = 10, so KMAX = 16) and on k = 7 tenants (KMAX = 8) -- replayed command by command on the
+oracle (oracle.bloom_stream = orc_bloom_stream: each command is add(T) / contains(T),
+M/RedissonBloomFilter.java:99-102,198-201, executed one after another).
+
+Per-command replies, both counts and every tenant bitmap (the Redis string, `GET name`) must be
+bit-identical.  Tenants are Zipf(s = 1)-skewed, 10% adds, the filters start at their design fill
+(random bitmaps imported as Redis strings, as bench.py's C5 leg does), and keys repeat so adds hit
+present keys and contains hit keys added earlier in the same chunk.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from redisson_amd import BloomHandle, bloom_stream
+from redisson_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _zipf_tenants(rng, nt, n, s=1.0):
+    w = 1.0 / np.arange(1, nt + 1, dtype=np.float64) ** s
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return np.minimum(np.searchsorted(cdf, rng.random(n)), nt - 1).astype(np.uint32)
+
+
+def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=0, klen=64):
+    rng = np.random.default_rng(seed)
+    names = [f"{fresh}-{t}" for t in range(nt)]
+    refs, handles = [], []
+    for nm in names:
+        f = client.getBloomFilter(nm)
+        assert f.tryInit(expected, fpp)
+        nb = (f.getSize() + 7) // 8
+        bm = rng.integers(0, 256, size=nb, dtype=np.uint8)  # design fill 0.5
+        f.importBitmap(bm.tobytes())
+        r = O.OracleBloom(f.getSize(), f.getHashIterations())
+        r.bitmap[:nb] = bm
+        r.redis_len = nb
+        refs.append(r)
+        handles.append(BloomHandle(client, nm))
+    kf = _zipf_tenants(rng, nt, n)
+    op = (rng.random(n) < 0.1).astype(np.uint8)
+    pool = rng.integers(0, 256, size=(n // 4, klen), dtype=np.uint8)
+    keys = pool[rng.integers(0, len(pool), size=n)]
+    # a contains right after the add of the same key on the same tenant, every 101 commands
+    idx = np.arange(0, n - 1, 101)
+    op[idx], op[idx + 1] = 1, 0
+    kf[idx + 1] = kf[idx]
+    keys[idx + 1] = keys[idx]
+    assert L.lib().rbx_tune(b"stream_chunk", chunk) == 0
+    assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
+    try:
+        out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
+    finally:
+        L.lib().rbx_tune(b"stream_chunk", 0)
+        L.lib().rbx_tune(b"stream_contains_slots", 0)
+    want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
+    bad = np.flatnonzero(out != want)
+    assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
+    assert [int(counts[0]), int(counts[1])] == wc
+    # the stream did real work: present contains and new adds on the hot tenants
+    assert wc[0] > 0 and wc[1] > 0
+    for nm, r in zip(names, refs):
+        assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
+    for h in handles:
+        h.close()
+    for nm in names:
+        client.getBloomFilter(nm).delete()
+    return wc
+
+
+def _fixed(keys):
+    from redisson_amd import Arena
+
+    return Arena.fixed(keys)
+
+
+def test_c5_instantiation_two_full_chunks(client, fresh):
+    """C5 exactly: tryInit(1e6, 1e-3) tenants (14,377,587 bits, k = 10 -> k_stream_*<64, 16>), 64-byte
+    keys, 7M commands = two chunks at the production chunk size (2^26 / 10 = 6,710,886 commands)."""
+    f = client.getBloomFilter(fresh + "-probe")
+    f.tryInit(1_000_000, 1e-3)
+    assert (f.getSize(), f.getHashIterations()) == (14_377_587, 10)
+    f.delete()
+    _c5_case(client, fresh, seed=0x5EED0005, nt=200, expected=1_000_000, fpp=1e-3, n=7_000_000)
+
+
+@pytest.mark.parametrize("slots", [0, 1])
+def test_c5_kmax8_many_chunks(client, fresh, slots):
+    """k = 7 tenants (tryInit(1e6, 0.01): 9,585,058 bits -> k_stream_*<64, 8>), 64-byte keys, 2M commands
+    in 300k-command chunks; both contains kernels (staged, per-lane slots)."""
+    _c5_case(client, fresh, seed=77 + slots, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000, chunk=300_000,
+             slots=slots)
+
+
+def test_c5_k10_chunk_boundaries(client, fresh):
+    """C5 tenants and keys in 303,031-command chunks (= 101 * 3000 + 1: the add at 303,030 and the
+    contains of the same key at 303,031 sit on the two sides of the first boundary; the earlier
+    chunk's commit must land before the next chunk probes)."""
+    _c5_case(client, fresh, seed=91, nt=100, expected=1_000_000, fpp=1e-3, n=2_000_000, chunk=303_031)

@@ -151,3 +151,50 @@ def test_node_and_single_context_agree(node, fresh):
         assert nf.containsEach(probe)[1].tolist() == cf.containsEach(probe)[1].tolist()
         assert nf.count() == cf.count()
     node.delete(fresh, "{" + fresh + "}:config")
+
+
+def test_contains_on_empty_filter_creates_no_bitmap(node, fresh):
+    """a node contains_multi on an initialized filter that was never added to reads all
+    zeros and creates no bitmap key (GETBIT creates nothing): DEL then counts only the config hash."""
+    import ctypes as C
+
+    nm = fresh + "-empty"
+    assert node.getBloomFilter(nm).tryInit(10_000, 0.01)
+    counts, pres = node.bloom_contains_multi([nm, nm], [0, 2, 3], Arena([b"a", b"b", b"c"]), per_key=True)
+    assert counts.tolist() == [0, 0] and not pres.any()
+    ctx = C.c_void_p()
+    assert L.lib().rbx_node_ctx(node.node, node.gpu_of(nm), C.byref(ctx)) == 0
+    e = C.c_int()
+    assert L.lib().rbx_bloom_is_exists(ctx, nm.encode(), C.byref(e)) == 0 and e.value == 0
+    assert node.delete(nm, "{" + nm + "}:config") == 1
+    # a single-context handle does not create it either
+    with RedissonClient(0) as c:
+        f = c.getBloomFilter(nm)
+        f.tryInit(10_000, 0.01)
+        from redisson_amd import BloomHandle
+
+        h = BloomHandle(c, nm)
+        assert f.contains(["a", "b"]) == 0
+        assert f.delete() is True  # config only; the bitmap never existed
+        h.close()
+
+
+def test_delete_releases_cached_handle_memory(node, fresh):
+    """the node caches one handle per (GPU, name); DEL evicts it, so a deleted tenant's
+    bitmap (here 120 MB, its own allocation past the 64 MiB slab limit) goes back to the device."""
+    import torch
+
+    nm = fresh + "-big"
+    assert node.getBloomFilter(nm).tryInit(100_000_000, 0.01)  # 958,505,837 bits = 120 MB
+    assert node.bloom_add_multi([nm], [0, 2], Arena([b"x", b"y"]))[0] == 2
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    assert node.delete(nm, "{" + nm + "}:config") == 2
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert free1 - free0 >= 100 << 20, (free0, free1)
+    # re-created with other parameters afterwards: a fresh handle is opened
+    assert node.getBloomFilter(nm).tryInit(1000, 0.01)
+    ref = O.OracleBloom(*O.bloom_optimal(1000, 0.01))
+    assert node.bloom_add_multi([nm], [0, 2], Arena([b"x", b"y"]))[0] == ref.add(*O.arena([b"x", b"y"]))
+    assert node.delete(nm, "{" + nm + "}:config") == 2

@@ -190,3 +190,40 @@ def test_multithreaded_restatement_matches_single_thread():
         r1 = a.contains(*O.fixed_arena(probe), per_key=True)
         r2 = b.contains_mt(*O.fixed_arena(probe), nthreads=5, per_key=True)
         assert r1[0] == r2[0] and np.array_equal(r1[1], r2[1])
+
+
+def test_stream_restatement_matches_per_key_batches():
+    """orc_bloom_stream (the C5 checker) == one add(T)/contains(T) batch per command, in order."""
+    rng = np.random.default_rng(1)
+    shapes = [(64, 7), (729, 5), (9585, 7), (-2000, 3)]
+    a = [O.OracleBloom(m, k) for m, k in shapes]
+    b = [O.OracleBloom(m, k) for m, k in shapes]
+    n = 4000
+    keys = rng.integers(0, 256, size=(n // 3, 16), dtype=np.uint8)[rng.integers(0, n // 3, size=n)]
+    kf = rng.integers(0, len(shapes), size=n).astype(np.uint32)
+    op = (rng.random(n) < 0.4).astype(np.uint8)
+    out, cnt = O.bloom_stream(a, kf, op, keys, None, stride=16)
+    want = np.array([(b[f].add if o else b[f].contains)(*O.fixed_arena(keys[i:i + 1]))
+                     for i, (f, o) in enumerate(zip(kf, op))], np.uint8)
+    assert np.array_equal(out, want)
+    assert cnt == [int(want[op == 0].sum()), int(want[op == 1].sum())]
+    assert all(x.redis_string() == y.redis_string() for x, y in zip(a, b))
+    # the arena form (variable-length keys) agrees with the fixed-stride form
+    c = [O.OracleBloom(m, k) for m, k in shapes]
+    out2, cnt2 = O.bloom_stream(c, kf, op, *O.fixed_arena(keys))
+    assert np.array_equal(out2, out) and cnt2 == cnt
+
+
+from bitset_vectors import BITSET_VECTORS, key_for_bit  # noqa: E402
+
+
+@pytest.mark.parametrize("bits,size_bits,card", BITSET_VECTORS)
+def test_bitset_vectors_on_oracle(bits, size_bits, card):
+    f = O.OracleBloom(64, 1)
+    keys = [key_for_bit(b) for b in bits]
+    assert f.add(*O.arena(keys)) == len(bits)  # every SETBIT returned 0 (testSetGet: set() is false)
+    assert f.redis_len * 8 == size_bits and f.bitcount() == card
+    s = f.redis_string()
+    got = [i for i in range(len(s) * 8) if s[i >> 3] & (0x80 >> (i & 7))]
+    assert got == sorted(bits)  # MSB-first: bit i is byte i >> 3, mask 0x80 >> (i & 7)
+    assert f.contains(*O.arena([key_for_bit(0)])) == (1 if 0 in bits else 0)  # get(0) is false
