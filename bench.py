@@ -12,8 +12,9 @@ Multi-GPU: one rank per GPU.  The driver launches N > 1 through torch.distribute
 WORLD_SIZE is unset and --gpus N > 1, bench.py launches those N ranks itself (a child
 torch.distributed.run, started before anything touches the GPU) and exits with its status.
 Every rank asserts WORLD_SIZE == --gpus.
-  - C2 does not shard ("replicas only"): every rank probes its own replica with its
-    own keys (weak scaling); `value` = keys of all ranks / max-over-ranks time.
+  - C2 does not shard ("replicas only"): every rank holds a replica of ONE filter (the
+    same adds, bitmap digests compared across ranks) and serves its own share of the contains
+    stream (weak scaling); `value` = keys of all ranks / max-over-ranks time.
   - leg C3 shards 100k tenant filters by CRC16 slot (slot * N / 16384, ClusterConnectionManager
     .java:814-830) with no data-path collective;
   - leg C4 partitions PFADD elements over the ranks and merges the 10k x 16384 partial registers
@@ -422,10 +423,15 @@ def run_c2(args, world, rank, local):
     f.tryInitRaw(SIZE, K)
     h = BloomHandle(client, "bench-c2")
 
+    # Replicas of ONE filter (SURVEY 8e "replicas only"): every rank adds the same keys (the same
+    # seed), so the bitmaps are identical -- checked below by a digest all-gather -- and each
+    # replica serves its own share of the contains stream (its present half is the added keys, its
+    # absent half is rank-specific).
     g = torch.Generator(device="cuda")
-    g.manual_seed(0x5EED0002 + 1000 * rank)
+    g.manual_seed(0x5EED0002)
     half = n // 2
     added = torch.randint(0, 256, (half, 32), dtype=torch.uint8, device="cuda", generator=g)
+    g.manual_seed(0x5EED0002 + 1000 * (rank + 1))
     fresh = torch.randint(0, 256, (n - half, 32), dtype=torch.uint8, device="cuda", generator=g)
     probe = torch.cat([added, fresh])
     del fresh
@@ -445,6 +451,10 @@ def run_c2(args, world, rank, local):
     with Timer(stream) as t_add:
         h.add_dev(device_keys(added.data_ptr(), half, 32), cnt.data_ptr(), stream=sptr)
     n_new = int(cnt[0].item())
+    # the replicas are one filter: equal digests of `GET bench-c2` on every rank
+    digest = f.digest()
+    digests = gather_over_ranks(world, digest - (1 << 64) if digest >= 1 << 63 else digest)
+    assert len(set(digests)) == 1 and digests[0] != 0, f"replicas differ: {digests}"
 
     dk = device_keys(probe.data_ptr(), n, 32)
     for _ in range(args.warmup):
@@ -517,10 +527,11 @@ def run_c2(args, world, rank, local):
         "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "C2 RBloomFilter.contains(Collection) of 100M random 32-byte keys "
+        "config": {"workload": f"C2 RBloomFilter.contains(Collection) of {n / 1e6:g}M random 32-byte keys "
                                "(50% present) vs one 2^32-bit k=7 filter per GPU",
                    "keys_per_gpu": n, "key_bytes": 32, "size_bits": SIZE, "k": K,
-                   "parallelism": f"replicas x{world} (no data-path collective)"},
+                   "parallelism": f"replicas x{world} of one filter (same adds on every rank, bitmap digests "
+                                  f"equal), contains keys split across replicas, no data-path collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
@@ -540,6 +551,7 @@ def run_c2(args, world, rank, local):
                      # working set (> 1: early exit and LDS probes avoid most random gathers)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
         "extra": {"add_keys_per_s_per_gpu": half / (t_add.ms / 1e3), "add_new_keys": n_new,
+                  "replica_digest": f"{digest:016x}", "replicas_identical": len(set(digests)) == 1,
                   "present_per_step": total_present // args.steps, "wall_s_timed": wall,
                   "contains_direct_kernel_ms": direct_ms,
                   "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3),
@@ -572,8 +584,9 @@ def run_c1(args, world, rank, local):
     sptr = stream.cuda_stream
     client = RedissonClient(local)
     g = torch.Generator(device="cuda")
-    g.manual_seed(0x5EED0001 + 1000 * rank)
+    g.manual_seed(0x5EED0001)  # replicas: the same adds on every rank, rank-specific absent probes
     keys = torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+    g.manual_seed(0x5EED0001 + 1000 * (rank + 1))
     probe = torch.cat([keys, torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)])
     cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
     t_add = t_con = 0.0

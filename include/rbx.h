@@ -196,6 +196,23 @@ int rbx_bloom_import(rbx_ctx *ctx, const char *name, const uint8_t *bytes, uint6
 /* SET name from a DEVICE buffer (device-resident snapshot restore); synchronous. */
 int rbx_bloom_import_dev(rbx_ctx *ctx, const char *name, const uint8_t *d_bytes, uint64_t len, void *stream);
 
+/* ---- replicas ("replicate the bitmap, split contains keys across GPUs") ---------
+ * Redisson serves contains' GETBITs as reads that may go to a replica
+ * (M/RedissonBitSet.java:277-279 readAsync, ReadMode.SLAVE M/config/BaseMasterSlaveServersConfig.java:60)
+ * and SETBITs to the master.  These are the engine's replica primitives. */
+/* Order-independent 64-bit digest of `GET name` (0 = missing key): equal replicas have equal
+ * digests (compared over a collective instead of moving the bitmaps). */
+int rbx_bloom_digest(rbx_ctx *ctx, const char *name, uint64_t *out);
+int rbx_bloom_digest_n(rbx_ctx *ctx, rbx_name name, uint64_t *out);
+/* Replica sync inside one process: dst's {name}:config and bitmap string := src's, copied
+ * device to device (hipMemcpyPeerAsync over xGMI between GPUs).  Key timeouts are not copied. */
+int rbx_bloom_copy_to(rbx_ctx *src, rbx_ctx *dst, rbx_name name);
+/* dst_name on dst := src_name on src (HLL registers, encoding, cached cardinality), device to
+ * device; a missing source deletes dst_name.  PFCOUNT / PFMERGE inputs from another GPU. */
+int rbx_hll_copy_to(rbx_ctx *src, rbx_name src_name, rbx_ctx *dst, rbx_name dst_name);
+/* Enables peer access from `device` to `peer` where the hardware allows (best effort). */
+int rbx_enable_peer_access(int device, int peer);
+
 /* ---- Bloom handles and the device-resident batch path ------------------------------ */
 int rbx_bloom_open(rbx_ctx *ctx, const char *name, rbx_bloom **out);
 int rbx_bloom_open_n(rbx_ctx *ctx, rbx_name name, rbx_bloom **out);
@@ -358,6 +375,15 @@ int rbx_node_bloom_contains(rbx_node *node, rbx_name name, uint64_t size, uint32
                             uint8_t *out_present, uint64_t *out_count);
 int rbx_node_bloom_count(rbx_node *node, rbx_name name, int64_t *out);
 int rbx_node_del(rbx_node *node, const rbx_name *names, uint32_t n, int *deleted);
+/* Replicated filter (SURVEY 8e, C2 "replicas only"): on != 0 copies the filter (config hash +
+ * bitmap) from its home GPU to every other GPU, device to device, then routes every add of it
+ * to all replicas (the home GPU's reply is returned) and spreads its contains over them (one
+ * key range per replica; multi-tenant segments round-robin) -- Redisson's reads-from-replicas
+ * (GETBIT via readAsync, M/RedissonBitSet.java:277-279; ReadMode.SLAVE,
+ * M/config/BaseMasterSlaveServersConfig.java:60).  on == 0 drops the copies.  DEL of the
+ * filter's keys deletes every copy; deleting its config ends the replication. */
+int rbx_node_bloom_replicate(rbx_node *node, rbx_name name, int on);
+int rbx_node_bloom_is_replicated(rbx_node *node, rbx_name name, int *replicated);
 /* segment s = keys [seg_offsets[s], seg_offsets[s+1]) of names[s] (host buffers; a segment must
  * be non-empty, as contains/add(Collection) of an empty collection throw); out_* nullable. */
 int rbx_node_bloom_contains_multi(rbx_node *node, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,

@@ -165,6 +165,14 @@ SIGNATURES = {
     "rbx_node_hll_add_multi": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p, C.POINTER(RbxKeys), u8p]),
     "rbx_node_hll_count": (C.c_int, [vp, C.POINTER(RbxName), C.c_uint32, u64p]),
     "rbx_node_hll_merge": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
+    "rbx_node_bloom_replicate": (C.c_int, [vp, RbxName, C.c_int]),
+    "rbx_node_bloom_is_replicated": (C.c_int, [vp, RbxName, C.POINTER(C.c_int)]),
+    # replicas
+    "rbx_bloom_digest": (C.c_int, [vp, C.c_char_p, u64p]),
+    "rbx_bloom_digest_n": (C.c_int, [vp, RbxName, u64p]),
+    "rbx_bloom_copy_to": (C.c_int, [vp, vp, RbxName]),
+    "rbx_hll_copy_to": (C.c_int, [vp, RbxName, vp, RbxName]),
+    "rbx_enable_peer_access": (C.c_int, [C.c_int, C.c_int]),
     "rbx_bench_slice_probe": (C.c_int, [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint, vp, vp]),
     "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
     "rbx_bench_stream_write": (C.c_int, [vp, vp, C.c_uint64, vp]),

@@ -285,6 +285,12 @@ class RBloomFilter(_Expirable):
         buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
         _check(L.lib().rbx_bloom_import(self._client.ctx, self._bname(), buf.ctypes.data_as(L.u8p), len(data)))
 
+    def digest(self) -> int:
+        """Order-independent 64-bit digest of `GET name` (0 = no bitmap): replica comparison."""
+        out = C.c_uint64()
+        _check(L.lib().rbx_bloom_digest(self._client.ctx, self._bname(), C.byref(out)))
+        return int(out.value)
+
     def bitcount(self) -> int:
         out = C.c_uint64()
         _check(L.lib().rbx_bloom_bitcount(self._client.ctx, self._bname(), C.byref(out)))

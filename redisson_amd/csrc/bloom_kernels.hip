@@ -1091,6 +1091,32 @@ __global__ __launch_bounds__(256) void k_bitcount(const uint8_t *__restrict__ by
     block_add_u64(c, out);
 }
 
+// Order-independent 64-bit digest of the Redis string's bytes: sum over 16-byte vectors v of
+// mix(v, position).  Replicas compare digests (one word per GPU over the collective) instead of
+// whole bitmaps.  The tail bytes past nbytes of the last vector are zero (bitmap invariant).
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 31;
+    x *= 0x7fb5d329728ea185ULL;
+    x ^= x >> 27;
+    x *= 0x81dadef4bc2dd44dULL;
+    x ^= x >> 33;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_digest(const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                                                unsigned long long *__restrict__ out) {
+    uint64_t d = 0;
+    const uint64_t nvec = (nbytes + 15) >> 4;
+    const uint4 *v = (const uint4 *)bytes;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        const uint4 x = ld_nt16(v + i);
+        const uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
+        d += mix64(lo ^ mix64(2 * i + 0x9E3779B97F4A7C15ULL)) + mix64(hi ^ mix64(2 * i + 1));
+    }
+    block_add_u64(d, out);
+}
+
 // ---------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------
@@ -1307,6 +1333,11 @@ void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st) {
     const unsigned grid = grid_for((nbytes + 15) / 16, kMaxGrid);
     hipLaunchKernelGGL(k_bitcount, dim3(grid), dim3(256), 0, st, bytes, nbytes, out);
+}
+
+void launch_digest(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st) {
+    const unsigned grid = grid_for((nbytes + 15) / 16, 4096);
+    hipLaunchKernelGGL(k_digest, dim3(grid), dim3(256), 0, st, bytes, nbytes, out);
 }
 
 }  // namespace rbx

@@ -2667,6 +2667,161 @@ int rbx_pexpiretime(rbx_ctx *c, const char *name, int64_t *out) {
     return ks_pexpiretime(c->ks, name, out);
 }
 
+// ---- replicas: digest and device-to-device copies between contexts ---------------------------
+// Waits until every engine call issued on `c` so far has finished on the device (the scratch
+// event chain orders them all, whatever stream each used), so its objects can be read elsewhere.
+static int quiesce(rbx_ctx *c) {
+    if (c->ev_scratch && c->scratch_stream) HIP_TRY(hipEventSynchronize(c->ev_scratch));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RBX_OK;
+}
+
+static uint64_t mix64_host(uint64_t x) {
+    x ^= x >> 31;
+    x *= 0x7fb5d329728ea185ULL;
+    x ^= x >> 27;
+    x *= 0x81dadef4bc2dd44dULL;
+    x ^= x >> 33;
+    return x;
+}
+
+int rbx_bloom_digest_n(rbx_ctx *c, rbx_name name, uint64_t *out) {
+    if (!c || (!name.bytes && name.len) || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->ks.mu);
+    RBX_TRY(set_device(c));
+    ScratchOrder so_(c, c->stream);
+    Entry *e = c->ks.find(name_of(name));
+    if (!e) {
+        *out = 0;  // a missing key (GET = nil)
+        return RBX_OK;
+    }
+    if (e->type != KType::Bitmap) return fail(RBX_E_WRONGTYPE, kWrongTypeMsg);
+    int rc;
+    const uint64_t len = read_dev_u64(c, e->bm->d_len, &rc);
+    RBX_TRY(rc);
+    RBX_TRY(c->counters.reserve(64));
+    auto *d = c->counters.as<unsigned long long>() + 4;
+    HIP_TRY(hipMemsetAsync(d, 0, 8, c->stream));
+    if (len) launch_digest((const uint8_t *)e->bm->d_words, len, d, c->stream);
+    HIP_TRY(hipGetLastError());
+    const uint64_t v = read_dev_u64(c, d, &rc);
+    RBX_TRY(rc);
+    *out = v + mix64_host(len ^ 0xD1B54A32D192ED03ULL) + 1;  // never 0 for an existing key
+    return RBX_OK;
+}
+
+int rbx_bloom_digest(rbx_ctx *c, const char *name, uint64_t *out) {
+    if (!name) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    return rbx_bloom_digest_n(c, rbx_name{(const uint8_t *)name, strlen(name)}, out);
+}
+
+// Replica sync of one Bloom filter: dst's {name}:config := src's (all four fields) and dst's
+// bitmap string := src's, copied device to device (hipMemcpyPeerAsync: xGMI between the GPUs of
+// a node, a plain device copy on one GPU).  The replica's key timeouts are not copied.
+int rbx_bloom_copy_to(rbx_ctx *src, rbx_ctx *dst, rbx_name name) {
+    if (!src || !dst || (!name.bytes && name.len)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    if (src == dst) return fail(RBX_E_ILLEGAL_ARGUMENT, "source and destination are the same context");
+    std::scoped_lock lk(src->ks.mu, dst->ks.mu);
+    const std::string nm = name_of(name);
+    RBX_TRY(set_device(src));
+    if (dst->shut) return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
+    BloomConfig cfg;
+    RBX_TRY(ks_get_config(src->ks, nm, &cfg));
+    RBX_TRY(check_offsets(cfg.size));
+    Entry *e = src->ks.find(nm);
+    if (e && e->type != KType::Bitmap) return fail(RBX_E_WRONGTYPE, kWrongTypeMsg);
+    std::shared_ptr<Bitmap> sb = e ? e->bm : nullptr;
+    uint64_t len = 0;
+    if (sb) {
+        RBX_TRY(quiesce(src));
+        int rc;
+        len = read_dev_u64(src, sb->d_len, &rc);
+        RBX_TRY(rc);
+    }
+    RBX_TRY(set_device(dst));
+    ScratchOrder so_(dst, dst->stream);
+    dst->ks.put(config_name(nm), Entry{KType::Config, std::make_shared<BloomConfig>(cfg), nullptr, nullptr});
+    dst->ks.generation++;
+    if (!sb) {  // the source has no bitmap yet: neither has the replica
+        dst->ks.erase(nm);
+        return RBX_OK;
+    }
+    const uint64_t bits = std::max<uint64_t>(size_bits(cfg.size), len * 8);
+    std::shared_ptr<Bitmap> b;
+    Entry *de = dst->ks.find(nm);
+    if (de && de->type == KType::Bitmap && de->bm->cap_bytes >= (bits + 7) / 8) {
+        b = de->bm;  // in place: the replica's open handles keep seeing it
+        HIP_TRY(hipMemsetAsync(b->d_words, 0, b->cap_bytes, dst->stream));
+    } else {
+        RBX_TRY(new_bitmap(dst, bits, dst->stream, &b));
+    }
+    if (len) HIP_TRY(hipMemcpyPeerAsync(b->d_words, dst->device, sb->d_words, src->device, len, dst->stream));
+    static thread_local unsigned long long L;
+    L = len;
+    HIP_TRY(hipMemcpyAsync(b->d_len, &L, 8, hipMemcpyHostToDevice, dst->stream));
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    dst->ks.put(nm, Entry{KType::Bitmap, nullptr, b, nullptr});
+    dst->ks.generation++;
+    return RBX_OK;
+}
+
+// PFMERGE's input from another GPU: dst_name on dst := src_name on src (registers, encoding,
+// cached cardinality and promotion word), device to device.  A missing source deletes dst_name.
+int rbx_hll_copy_to(rbx_ctx *src, rbx_name src_name, rbx_ctx *dst, rbx_name dst_name) {
+    if (!src || !dst || (!src_name.bytes && src_name.len) || (!dst_name.bytes && dst_name.len))
+        return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    const std::string sn = name_of(src_name), dn = name_of(dst_name);
+    if (src == dst && sn == dn) return RBX_OK;
+    std::unique_lock<std::recursive_mutex> l1(src->ks.mu, std::defer_lock), l2(dst->ks.mu, std::defer_lock);
+    if (src == dst) l1.lock();
+    else std::lock(l1, l2);
+    RBX_TRY(set_device(src));
+    if (dst->shut) return fail(RBX_E_ILLEGAL_STATE, "the context has been shut down");
+    Entry *e = src->ks.find(sn);
+    if (e && e->type != KType::Hll) return fail(RBX_E_WRONGTYPE, kHllWrongType);
+    if (!e) {
+        dst->ks.erase(dn);
+        return RBX_OK;
+    }
+    std::shared_ptr<HllState> sh = e->hll;
+    RBX_TRY(quiesce(src));
+    RBX_TRY(set_device(dst));
+    ScratchOrder so_(dst, dst->stream);
+    Entry *de = dst->ks.find(dn);
+    if (de && de->type != KType::Hll) {
+        dst->ks.erase(dn);
+        de = nullptr;
+    }
+    std::shared_ptr<HllState> h;
+    if (de) {
+        h = de->hll;
+        de->expire_at = -1;  // SET semantics
+    } else {
+        RBX_TRY(hll_alloc(dst, dst->stream, &h));
+        dst->ks.put(dn, Entry{KType::Hll, nullptr, nullptr, h});
+        dst->ks.generation++;
+    }
+    h->card = sh->card;
+    h->dense = sh->dense;
+    HIP_TRY(hipMemcpyPeerAsync(h->d_regs, dst->device, sh->d_regs, src->device, kHllBytes, dst->stream));
+    HIP_TRY(hipMemcpyPeerAsync(h->d_promoted, dst->device, sh->d_promoted, src->device, 4, dst->stream));
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    return RBX_OK;
+}
+
+// Peer access between the GPUs of a node (best effort: copies work without it, staged).
+int rbx_enable_peer_access(int device, int peer) {
+    if (device == peer) return RBX_OK;
+    int can = 0;
+    HIP_TRY(hipDeviceCanAccessPeer(&can, device, peer));
+    if (!can) return RBX_OK;
+    HIP_TRY(hipSetDevice(device));
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(RBX_E_DEVICE, hipGetErrorString(e));
+    (void)hipGetLastError();
+    return RBX_OK;
+}
+
 // Tuning knobs (process-wide).  "contains_stage1": early-exit width of contains (0 = off).
 int rbx_tune(const char *key, int value) {
     if (!key) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key");

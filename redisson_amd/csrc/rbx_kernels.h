@@ -158,6 +158,8 @@ void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const Filte
                                  uint8_t *out, unsigned long long *counts, hipStream_t st, bool slots);
 void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
+// order-independent digest of a Redis string's bytes (replica comparison); *out += digest
+void launch_digest(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
 // region-local gathers: 6 loads per lane inside XCD-assigned regions (partitioned-probe roofline)
 void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region_words, uint64_t total_lanes,
                            uint32_t *sink, hipStream_t st, unsigned grid);

@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,9 +41,18 @@ constexpr size_t kMaxCachedHandles = 1u << 20;
 
 struct rbx_node {
     std::vector<rbx_ctx *> ctx;
-    std::mutex mu;                                           // the handle cache
+    std::mutex mu;                                           // the handle cache and the replica set
     std::map<std::pair<int, std::string>, HandleRef> blooms;  // open handles per (GPU, name)
+    // Bloom filters replicated on every GPU (rbx_node_bloom_replicate): adds go to every replica,
+    // contains are spread over them (Redisson's ReadMode.SLAVE reads,
+    // M/config/BaseMasterSlaveServersConfig.java:60; GETBIT is a read, M/RedissonBitSet.java:277-279)
+    std::set<std::string> replicated;
 };
+
+static bool is_replicated(rbx_node *nd, const std::string &name) {
+    std::lock_guard<std::mutex> lk(nd->mu);
+    return nd->replicated.count(name) != 0;
+}
 
 static std::atomic<uint64_t> g_tmp_serial{1};
 
@@ -93,6 +103,10 @@ extern "C" {
 
 int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
     if (!out || n_gpus < 1 || n_gpus > 16384) return fail(RBX_E_ILLEGAL_ARGUMENT, "n_gpus must be in [1, 16384]");
+    // replica syncs and cross-GPU HLL inputs are peer copies over xGMI
+    for (int i = 0; i < n_gpus; ++i)
+        for (int j = 0; j < n_gpus; ++j)
+            (void)rbx_enable_peer_access(devices ? devices[i] : i, devices ? devices[j] : j);
     auto *nd = new rbx_node();
     for (int i = 0; i < n_gpus; ++i) {
         rbx_ctx *c = nullptr;
@@ -153,18 +167,92 @@ int rbx_node_bloom_read_config(rbx_node *nd, rbx_name name, rbx_bloom_config *ou
     return rbx_bloom_read_config_n(nd->ctx[gpu_of(nd, str_of(name))], name, out);
 }
 
+static std::vector<int> all_gpus(const rbx_node *nd) {
+    std::vector<int> g(nd->ctx.size());
+    for (size_t i = 0; i < g.size(); ++i) g[i] = (int)i;
+    return g;
+}
+
+// A replicated filter's add is applied to every replica (the same batch in the same order on
+// each, so they stay identical); the reply is the home GPU's.
 int rbx_node_bloom_add(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
                        uint8_t *out_new, uint64_t *out_count) {
     if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
     NODE_TRY(check_name(name));
-    return rbx_bloom_add_n(nd->ctx[gpu_of(nd, str_of(name))], name, size, k, keys, out_new, out_count);
+    const std::string nm = str_of(name);
+    const int home = gpu_of(nd, nm);
+    if (!is_replicated(nd, nm) || nd->ctx.size() == 1)
+        return rbx_bloom_add_n(nd->ctx[home], name, size, k, keys, out_new, out_count);
+    return per_gpu(all_gpus(nd), [&](int g) -> int {
+        uint64_t cnt = 0;
+        return rbx_bloom_add_n(nd->ctx[g], name, size, k, keys, g == home ? out_new : nullptr,
+                               g == home ? out_count : &cnt);
+    });
 }
 
+// A replicated filter's contains is split into one contiguous key range per replica, run
+// concurrently; flags land in key order and the count is the sum.
 int rbx_node_bloom_contains(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
                             uint8_t *out_present, uint64_t *out_count) {
     if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
     NODE_TRY(check_name(name));
-    return rbx_bloom_contains_n(nd->ctx[gpu_of(nd, str_of(name))], name, size, k, keys, out_present, out_count);
+    const std::string nm = str_of(name);
+    const int home = gpu_of(nd, nm);
+    const uint64_t N = nd->ctx.size();
+    if (!keys || keys->n < N || !is_replicated(nd, nm) || N == 1)
+        return rbx_bloom_contains_n(nd->ctx[home], name, size, k, keys, out_present, out_count);
+    if (keys->n && !keys->bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
+    std::vector<uint64_t> cnt(N, 0);
+    NODE_TRY(per_gpu(all_gpus(nd), [&](int g) -> int {
+        const uint64_t i0 = keys->n * (uint64_t)g / N, i1 = keys->n * (uint64_t)(g + 1) / N;
+        rbx_keys sub = keys->offsets ? rbx_keys{keys->bytes, keys->offsets + i0, 0, i1 - i0}
+                                     : rbx_keys{keys->bytes + i0 * keys->stride, nullptr, keys->stride, i1 - i0};
+        return rbx_bloom_contains_n(nd->ctx[g], name, size, k, &sub, out_present ? out_present + i0 : nullptr,
+                                    &cnt[g]);
+    }));
+    if (out_count) {
+        uint64_t t = 0;
+        for (uint64_t c : cnt) t += c;
+        *out_count = t;
+    }
+    return RBX_OK;
+}
+
+// on != 0: copies the filter (config hash + bitmap) from its home GPU to every other GPU, device
+// to device, and from then on routes adds to all replicas and spreads contains over them.
+// on == 0: drops the copies (the home GPU keeps the filter).
+int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
+    if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
+    NODE_TRY(check_name(name));
+    const std::string nm = str_of(name), cn = config_name(nm);
+    const int home = gpu_of(nd, nm);
+    std::vector<int> others;
+    for (int g = 0; g < (int)nd->ctx.size(); ++g)
+        if (g != home) others.push_back(g);
+    if (on) {
+        rbx_bloom_config cfg;
+        NODE_TRY(rbx_bloom_read_config_n(nd->ctx[home], name, &cfg));  // not initialized: ISE
+        NODE_TRY(per_gpu(others, [&](int g) -> int { return rbx_bloom_copy_to(nd->ctx[home], nd->ctx[g], name); }));
+        std::lock_guard<std::mutex> lk(nd->mu);
+        nd->replicated.insert(nm);
+        return RBX_OK;
+    }
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        nd->replicated.erase(nm);
+    }
+    const rbx_name both[2] = {name, name_ref(cn)};
+    return per_gpu(others, [&](int g) -> int {
+        int d;
+        return rbx_del_n(nd->ctx[g], both, 2, &d);
+    });
+}
+
+int rbx_node_bloom_is_replicated(rbx_node *nd, rbx_name name, int *out) {
+    if (!nd || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    NODE_TRY(check_name(name));
+    *out = is_replicated(nd, str_of(name)) ? 1 : 0;
+    return RBX_OK;
 }
 
 int rbx_node_bloom_count(rbx_node *nd, rbx_name name, int64_t *out) {
@@ -173,22 +261,53 @@ int rbx_node_bloom_count(rbx_node *nd, rbx_name name, int64_t *out) {
     return rbx_bloom_count_n(nd->ctx[gpu_of(nd, str_of(name))], name, out);
 }
 
+// the filters a key name can belong to: `key` itself, or every `name` with
+// suffixName(name, "config") == key -- "{name}:config", or "name:config" for a name holding a '{'
+// (M/RedissonObject.java:77-82; "X" and "{X}" share the config key "{X}:config")
+static std::vector<std::string> filters_of(const std::string &key) {
+    std::vector<std::string> out{key};
+    const std::string sfx = ":config";
+    if (key.size() <= sfx.size() || key.compare(key.size() - sfx.size(), sfx.size(), sfx) != 0) return out;
+    const std::string plain = key.substr(0, key.size() - sfx.size());
+    if (config_name(plain) == key) out.push_back(plain);
+    if (plain.size() >= 2 && plain.front() == '{' && plain.back() == '}') {
+        const std::string inner = plain.substr(1, plain.size() - 2);
+        if (config_name(inner) == key) out.push_back(inner);
+    }
+    return out;
+}
+
 int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) {
     if (!nd || (n && !names)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     std::vector<std::vector<rbx_name>> by(nd->ctx.size());
+    std::vector<std::vector<rbx_name>> replica_keys(nd->ctx.size());  // copies: not counted
     for (uint32_t i = 0; i < n; ++i) {
         NODE_TRY(check_name(names[i]));
-        by[gpu_of(nd, str_of(names[i]))].push_back(names[i]);
+        const std::string key = str_of(names[i]);
+        const int home = gpu_of(nd, key);
+        by[home].push_back(names[i]);
+        std::lock_guard<std::mutex> lk(nd->mu);
+        bool repl = false;
+        for (const std::string &f : filters_of(key)) {
+            if (!nd->replicated.count(f)) continue;
+            repl = true;
+            if (f != key) nd->replicated.erase(f);  // the config is gone: the filter is gone
+        }
+        if (repl)
+            for (size_t g = 0; g < nd->ctx.size(); ++g)
+                if ((int)g != home) replica_keys[g].push_back(names[i]);
     }
     // the deleted names' cached handles go too (each holds its bitmap until its next call)
     std::vector<HandleRef> evicted;
     {
         std::lock_guard<std::mutex> lk(nd->mu);
         for (uint32_t i = 0; i < n; ++i) {
-            auto it = nd->blooms.find(std::make_pair(gpu_of(nd, str_of(names[i])), str_of(names[i])));
-            if (it != nd->blooms.end()) {
-                evicted.push_back(std::move(it->second));
-                nd->blooms.erase(it);
+            for (int g = 0; g < (int)nd->ctx.size(); ++g) {  // replicas are cached on every GPU
+                auto it = nd->blooms.find(std::make_pair(g, str_of(names[i])));
+                if (it != nd->blooms.end()) {
+                    evicted.push_back(std::move(it->second));
+                    nd->blooms.erase(it);
+                }
             }
         }
     }
@@ -200,6 +319,11 @@ int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) 
         NODE_TRY(rbx_del_n(nd->ctx[g], by[g].data(), (uint32_t)by[g].size(), &d));
         total += d;
     }
+    for (size_t g = 0; g < replica_keys.size(); ++g) {
+        if (replica_keys[g].empty()) continue;
+        int d = 0;
+        NODE_TRY(rbx_del_n(nd->ctx[g], replica_keys[g].data(), (uint32_t)replica_keys[g].size(), &d));
+    }
     if (deleted) *deleted = total;
     return RBX_OK;
 }
@@ -208,6 +332,7 @@ int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) 
 // One GPU's share of a batch: its segments (in batch order) copied into a host arena.
 struct Part {
     std::vector<uint32_t> segs;  // batch segment ids
+    std::vector<uint8_t> primary;  // 1: this GPU's reply is the segment's (0: a replica's copy)
     std::vector<uint8_t> bytes;
     std::vector<uint64_t> offs;  // variable-length arenas
     std::vector<uint64_t> seg;   // local segment offsets
@@ -227,11 +352,30 @@ static int validate_batch(const rbx_name *names, uint32_t nseg, const uint64_t *
     return RBX_OK;
 }
 
-// scatter: every GPU's part of the batch, keys copied in segment order
+// scatter: every GPU's part of the batch, keys copied in segment order.  Segment s runs on its
+// name's home GPU; with `repl` (replicated names, Bloom only) an add segment also runs on every
+// other GPU (its reply discarded) and a contains segment runs on GPU (home + s) % N instead.
 static void build_parts(const rbx_node *nd, const std::vector<std::string> &sn, const uint64_t *seg,
-                        const rbx_keys *keys, std::vector<Part> *parts) {
-    parts->assign(nd->ctx.size(), Part{});
-    for (uint32_t s = 0; s < sn.size(); ++s) (*parts)[gpu_of(nd, sn[s])].segs.push_back(s);
+                        const rbx_keys *keys, std::vector<Part> *parts, const std::vector<uint8_t> *repl = nullptr,
+                        bool is_add = false) {
+    const int N = (int)nd->ctx.size();
+    parts->assign(N, Part{});
+    for (uint32_t s = 0; s < sn.size(); ++s) {
+        const int home = gpu_of(nd, sn[s]);
+        if (!repl || !(*repl)[s]) {
+            (*parts)[home].segs.push_back(s);
+            (*parts)[home].primary.push_back(1);
+        } else if (!is_add) {
+            const int g = (home + (int)(s % (uint32_t)N)) % N;
+            (*parts)[g].segs.push_back(s);
+            (*parts)[g].primary.push_back(1);
+        } else {
+            for (int g = 0; g < N; ++g) {
+                (*parts)[g].segs.push_back(s);
+                (*parts)[g].primary.push_back(g == home);
+            }
+        }
+    }
     for (Part &p : *parts) {
         if (p.segs.empty()) continue;
         p.seg.push_back(0);
@@ -295,8 +439,14 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
     NODE_TRY(validate_batch(names, nseg, seg, keys));
     std::vector<std::string> sn(nseg);
     for (uint32_t s = 0; s < nseg; ++s) sn[s] = str_of(names[s]);
+    std::vector<uint8_t> repl(nseg, 0);
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        if (!nd->replicated.empty())
+            for (uint32_t s = 0; s < nseg; ++s) repl[s] = nd->replicated.count(sn[s]) != 0;
+    }
     std::vector<Part> parts;
-    build_parts(nd, sn, seg, keys, &parts);
+    build_parts(nd, sn, seg, keys, &parts, &repl, is_add);
     const std::vector<int> gpus = gpus_with_work(parts);
     const int rc = per_gpu(gpus, [&](int g) -> int {
         Part &p = parts[g];
@@ -318,6 +468,7 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
     for (int g : gpus) {
         const Part &p = parts[g];
         for (size_t j = 0; j < p.segs.size(); ++j) {
+            if (!p.primary[j]) continue;
             const uint32_t s = p.segs[j];
             if (counts) counts[s] = p.cnt[j];
             if (out) memcpy(out + seg[s], p.out.data() + p.seg[j], seg[s + 1] - seg[s]);
@@ -361,19 +512,20 @@ int rbx_node_hll_add_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, c
     return RBX_OK;
 }
 
-// Names of other GPUs' HLLs as temporary keys on GPU `dst`: their Redis strings (encoding kept)
-// exported and imported there.  Missing keys are skipped (PFCOUNT / PFMERGE ignore them).
+// Names of other GPUs' HLLs as temporary keys on GPU `dst`: their registers (with encoding and
+// cached cardinality) copied device to device (rbx_hll_copy_to: a peer copy over xGMI, no host
+// staging).  Missing keys are skipped (PFCOUNT / PFMERGE ignore them).
 static int stage_on(rbx_node *nd, int dst, const std::vector<std::string> &remote, std::vector<std::string> *tmps) {
-    std::vector<uint8_t> buf(16 + 12288);
     for (const std::string &r : remote) {
-        uint64_t len = 0;
-        NODE_TRY(rbx_hll_export_enc_n(nd->ctx[gpu_of(nd, r)], name_ref(r), RBX_HLL_AS_STORED, buf.data(), buf.size(),
-                                      &len));
-        if (len == 0) continue;
+        int ex = 0;
+        const rbx_name rn = name_ref(r);
+        const int g = gpu_of(nd, r);
+        NODE_TRY(rbx_exists_n(nd->ctx[g], &rn, 1, &ex));
+        if (!ex) continue;
         // a binary name no client key is expected to take: NUL-prefixed, unique per call
         std::string t = std::string("\0rbx-node-tmp:", 14) + std::to_string(g_tmp_serial++);
-        NODE_TRY(rbx_hll_import_n(nd->ctx[dst], name_ref(t), buf.data(), len));
         tmps->push_back(t);
+        NODE_TRY(rbx_hll_copy_to(nd->ctx[g], rn, nd->ctx[dst], name_ref(t)));
     }
     return RBX_OK;
 }

@@ -129,6 +129,21 @@ class NodeBloomFilter:
                   C.byref(cnt)))
         return (int(cnt.value), out[: a.n]) if flags else int(cnt.value)
 
+    def replicate(self, on: bool = True) -> None:
+        """Copy the filter to every GPU of the node (adds go to all replicas, contains are spread
+        over them) -- or drop the copies (rbx_node_bloom_replicate)."""
+        s, keep = self._n()
+        _check(L.lib().rbx_node_bloom_replicate(self._node.node, s, 1 if on else 0))
+
+    def isReplicated(self) -> bool:
+        s, keep = self._n()
+        r = C.c_int()
+        _check(L.lib().rbx_node_bloom_is_replicated(self._node.node, s, C.byref(r)))
+        return bool(r.value)
+
+    def addEach(self, objects):
+        return self._batch(L.lib().rbx_node_bloom_add, objects, True)
+
     def add(self, objects):
         if isinstance(objects, Arena) or _is_collection(objects):
             return self._batch(L.lib().rbx_node_bloom_add, objects, False)

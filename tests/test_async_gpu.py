@@ -115,7 +115,7 @@ def test_async_submit_races_shutdown():
     # an open handle keeps the context object alive past rbx_shutdown (calls then fail cleanly)
     hold = C.c_void_p()
     assert L.lib().rbx_hll_open(ctx, b"race", 1, C.byref(hold)) == 0
-    accepted, refused, lock = [], [], threading.Lock()
+    accepted, refused, outs, lock = [], [], [], threading.Lock()
     keys = Arena([b"a", b"b", b"c"])
 
     def submitter():
@@ -125,6 +125,7 @@ def test_async_submit_races_shutdown():
             rc = L.lib().rbx_hll_add_async(ctx, b"race", keys.ptr(), C.byref(changed), None, None, C.byref(fp))
             with lock:
                 (accepted if rc == 0 else refused).append(fp if rc == 0 else rc)
+                outs.append(changed)  # written when the call runs: must outlive it
 
     th = [threading.Thread(target=submitter) for _ in range(4)]
     for t in th:
@@ -158,12 +159,13 @@ def test_shutdown_from_completion_callback():
 
     cb = CB(on_done)
     keys = Arena([b"k"])
-    futs = []
+    futs, outs = [], []
     for i in range(1, 6):
         fp = C.c_void_p()
         changed = C.c_int()
         assert L.lib().rbx_hll_add_async(ctx, b"cbshut", keys.ptr(), C.byref(changed), C.cast(cb, C.c_void_p),
                                          C.c_void_p(i), C.byref(fp)) in (0, L.RBX_E_ILLEGAL_STATE)
+        outs.append(changed)  # written when the call runs: must outlive it
         if fp.value:
             futs.append(fp)
     rcs = _wait_all(futs)

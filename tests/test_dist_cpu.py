@@ -156,3 +156,29 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+
+
+def _replica_digests(rank, world):
+    """bench.py's C2 replica rule on the oracle: every rank adds the keys of ONE seed, so the
+    replicas' Redis strings are identical and the digest all-gather agrees; rank-specific adds (the
+    r02 bench) would not be one filter, and the same check catches it."""
+    import hashlib
+
+    import bench
+
+    def digest(f):
+        return int.from_bytes(hashlib.blake2b(f.redis_string(), digest_size=8).digest(), "little") >> 1
+
+    keys = np.random.default_rng(0x5EED0002).integers(0, 256, size=(20_000, 32), dtype=np.uint8)
+    f = O.OracleBloom(1 << 20, 7)
+    f.add(*O.fixed_arena(keys))
+    ds = bench.gather_over_ranks(world, digest(f))
+    assert len(set(ds)) == 1
+    own = np.random.default_rng(0x5EED0002 + 1000 * (rank + 1)).integers(0, 256, size=(20_000, 32), dtype=np.uint8)
+    g = O.OracleBloom(1 << 20, 7)
+    g.add(*O.fixed_arena(own))
+    assert len(set(bench.gather_over_ranks(world, digest(g)))) == world
+
+
+def test_c2_replicas_are_one_filter_gloo():
+    _run(_replica_digests)

@@ -165,7 +165,8 @@ def test_contains_on_empty_filter_creates_no_bitmap(node, fresh):
     ctx = C.c_void_p()
     assert L.lib().rbx_node_ctx(node.node, node.gpu_of(nm), C.byref(ctx)) == 0
     e = C.c_int()
-    assert L.lib().rbx_bloom_is_exists(ctx, nm.encode(), C.byref(e)) == 0 and e.value == 0
+    arr, keep = L.names_array([nm])  # EXISTS name (the bitmap key)
+    assert L.lib().rbx_exists_n(ctx, arr, 1, C.byref(e)) == 0 and e.value == 0
     assert node.delete(nm, "{" + nm + "}:config") == 1
     # a single-context handle does not create it either
     with RedissonClient(0) as c:
@@ -198,3 +199,165 @@ def test_delete_releases_cached_handle_memory(node, fresh):
     ref = O.OracleBloom(*O.bloom_optimal(1000, 0.01))
     assert node.bloom_add_multi([nm], [0, 2], Arena([b"x", b"y"]))[0] == ref.add(*O.arena([b"x", b"y"]))
     assert node.delete(nm, "{" + nm + "}:config") == 2
+
+
+def _ctx(node, g):
+    import ctypes as C
+
+    ctx = C.c_void_p()
+    assert L.lib().rbx_node_ctx(node.node, g, C.byref(ctx)) == 0
+    return ctx
+
+
+def _export(ctx, nm, nbytes):
+    import ctypes as C
+
+    buf = np.zeros(nbytes + 1, np.uint8)
+    n = C.c_uint64()
+    assert L.lib().rbx_bloom_export(ctx, nm.encode(), buf.ctypes.data_as(L.u8p), buf.size, C.byref(n)) == 0
+    return buf[: n.value].tobytes()
+
+
+def _digest(ctx, nm):
+    import ctypes as C
+
+    d = C.c_uint64()
+    assert L.lib().rbx_bloom_digest(ctx, nm.encode(), C.byref(d)) == 0
+    return d.value
+
+
+def test_replicated_filter(node, fresh):
+    """SURVEY 8e for C2 ("replicas only"): a filter replicated on every GPU of the node.  The copy is
+    device to device (rbx_bloom_copy_to); afterwards every add reaches every replica and contains are
+    split across them -- replies per key equal the oracle's, all replicas stay byte-identical (equal
+    Redis strings and digests), multi-tenant batches naming the filter follow the same rules, and DEL
+    removes every copy."""
+    rng = np.random.default_rng(44)
+    nm, other = fresh + "-rep", fresh + "-solo"
+    f = node.getBloomFilter(nm)
+    assert f.tryInit(200_000, 0.01)
+    ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+    nbytes = (f.getSize() + 7) // 8
+    k1 = [rng.bytes(int(x)) for x in rng.integers(1, 40, size=20_000)]
+    assert f.add(k1) == ref.add(*O.arena(k1))  # home GPU only
+    assert not f.isReplicated()
+    f.replicate()
+    assert f.isReplicated()
+
+    def all_equal():
+        want = ref.redis_string()
+        digests = set()
+        for g in range(N):
+            assert _export(_ctx(node, g), nm, nbytes) == want, g
+            digests.add(_digest(_ctx(node, g), nm))
+        assert len(digests) == 1 and 0 not in digests
+
+    all_equal()
+    k2 = k1[:5000] + [rng.bytes(24) for _ in range(30_000)]
+    c, new = f.addEach(k2)
+    cr, nr = ref.add(*O.arena(k2), per_key=True)
+    assert c == cr and np.array_equal(new, nr)
+    all_equal()
+    probe = k2[::3] + [rng.bytes(24) for _ in range(40_000)]
+    cp, pres = f.containsEach(probe)
+    crp, pr = ref.contains(*O.arena(probe), per_key=True)
+    assert cp == crp and np.array_equal(pres, pr)
+    # multi-tenant batches naming the replicated filter (adds to every replica, contains spread)
+    assert node.getBloomFilter(other).tryInit(10_000, 0.01)
+    oref = O.OracleBloom(*O.bloom_optimal(10_000, 0.01))
+    k3 = [rng.bytes(16) for _ in range(3000)]
+    seg = np.array([0, 1000, 1500, 3000], np.uint64)
+    counts, flags = node.bloom_add_multi([nm, other, nm], seg, Arena(k3), per_key=True)
+    for s, r in enumerate([ref, oref, ref]):
+        cc, ff = r.add(*O.arena(k3[seg[s]:seg[s + 1]]), per_key=True)
+        assert counts[s] == cc and np.array_equal(flags[seg[s]:seg[s + 1]], ff)
+    all_equal()
+    names = [nm, other] + [nm] * 6
+    seg = np.arange(len(names) + 1, dtype=np.uint64) * np.uint64(500)
+    k4 = [k3[int(i)] if rng.random() < 0.5 else rng.bytes(16) for i in rng.integers(0, 3000, size=int(seg[-1]))]
+    counts, flags = node.bloom_contains_multi(names, seg, Arena(k4), per_key=True)
+    for s, n_ in enumerate(names):
+        r = ref if n_ == nm else oref
+        cc, ff = r.contains(*O.arena(k4[seg[s]:seg[s + 1]]), per_key=True)
+        assert counts[s] == cc and np.array_equal(flags[seg[s]:seg[s + 1]], ff)
+    assert f.count() == ref.count()
+    # DEL removes every copy and ends the replication
+    assert node.delete(nm, "{" + nm + "}:config", other, "{" + other + "}:config") == 4
+    assert not f.isReplicated()
+    import ctypes as C
+
+    for g in range(N):
+        e = C.c_int()
+        names_, keep = L.names_array([nm, "{" + nm + "}:config"])
+        assert L.lib().rbx_exists_n(_ctx(node, g), names_, 2, C.byref(e)) == 0 and e.value == 0, g
+
+
+def test_bloom_copy_between_contexts_and_digest(fresh):
+    """rbx_bloom_copy_to between two contexts (the replica-sync primitive): config hash (all four
+    fields) and bitmap string arrive byte-identical; the digest tells equal from different."""
+    import ctypes as C
+
+    rng = np.random.default_rng(45)
+    with RedissonClient(0) as a, RedissonClient(0) as b:
+        fa = a.getBloomFilter(fresh)
+        assert fa.tryInit(1_000_000, 1e-3)
+        keys = [rng.bytes(32) for _ in range(50_000)]
+        fa.add(keys)
+        assert b.getBloomFilter(fresh).digest() == 0  # missing key
+        nm = L.name_struct(fresh)
+        assert L.lib().rbx_bloom_copy_to(a.ctx, b.ctx, nm[0]) == 0
+        fb = b.getBloomFilter(fresh)
+        assert (fb.getSize(), fb.getHashIterations(), fb.getExpectedInsertions(), fb.getFalseProbability()) == \
+            (fa.getSize(), fa.getHashIterations(), 1_000_000, 1e-3)
+        assert fb.exportBitmap() == fa.exportBitmap() and fb.digest() == fa.digest() != 0
+        assert fb.contains(keys) == len(keys)
+        fb.add([b"only-on-b"])
+        assert fb.digest() != fa.digest()
+        assert L.lib().rbx_bloom_copy_to(a.ctx, b.ctx, nm[0]) == 0  # re-sync in place
+        assert fb.digest() == fa.digest()
+        assert L.lib().rbx_bloom_copy_to(a.ctx, a.ctx, nm[0]) == L.RBX_E_ILLEGAL_ARGUMENT
+        missing = L.name_struct(fresh + "-none")
+        assert L.lib().rbx_bloom_copy_to(a.ctx, b.ctx, missing[0]) == L.RBX_E_ILLEGAL_STATE
+        fa.delete()
+        fb.delete()
+
+
+def test_cross_gpu_hll_union_keeps_encodings(node, fresh):
+    """Cross-GPU PFCOUNT / PFMERGE stage remote HLLs by device copies (rbx_hll_copy_to): a merge of
+    sparse-only inputs stays sparse and one dense input makes it dense, as Redis PFMERGE does."""
+    import ctypes as C
+
+    rng = np.random.default_rng(46)
+    names = [f"{fresh}-s{i}" for i in range(6)]
+    assert len({node.gpu_of(n) for n in names}) > 1
+    regs = []
+    for i, nm in enumerate(names):
+        el = rng.integers(0, 256, size=(50 if i < 5 else 20_000, 16), dtype=np.uint8)
+        node.getHyperLogLog(nm).addAll([bytes(x) for x in el])
+        r = O.hll_new()
+        O.hll_pfadd(r, *O.fixed_arena(el))
+        regs.append(r)
+
+    def stored(nm):
+        ctx = _ctx(node, node.gpu_of(nm))
+        buf = np.zeros(16 + 12288, np.uint8)
+        n = C.c_uint64()
+        s, keep = L.name_struct(nm)
+        assert L.lib().rbx_hll_export_enc_n(ctx, s, 2, buf.ctypes.data_as(L.u8p), buf.size,  # AS_STORED
+                                            C.byref(n)) == 0
+        return buf[: n.value].tobytes()
+
+    u = O.hll_new()
+    for r in regs[:5]:
+        O.hll_merge(u, r)
+    d1 = fresh + "-d1"
+    node.getHyperLogLog(d1).mergeWith(*names[:5])
+    s1 = stored(d1)
+    assert s1[4] == 1 and np.array_equal(O.hll_sparse_unpack(s1[16:]), u)  # sparse
+    d2 = fresh + "-d2"
+    node.getHyperLogLog(d2).mergeWith(*names)
+    O.hll_merge(u, regs[5])
+    s2 = stored(d2)
+    assert s2[4] == 0 and np.array_equal(O.hll_dense_unpack(s2[16:]), u)  # dense
+    assert node.getHyperLogLog(names[0]).countWith(*names[1:]) == O.hll_count(u)
+    assert node.delete(*names, d1, d2) == len(names) + 2
