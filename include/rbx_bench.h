@@ -22,6 +22,10 @@ int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_b
  * b * slice_bytes (a power of two); workgroups take buckets by blockIdx % 8 (XCD affinity). */
 int rbx_bench_slice_probe(rbx_ctx *ctx, const void *d_entries, uint64_t per_bucket, uint32_t nbuckets,
                           const void *d_bitmap, uint64_t slice_bytes, unsigned grid, void *d_sink, void *stream);
+/* Region-pass phase times of the partitioned add, summed over every block's wave 0 since the
+ * last read (s_memtime ticks; collected only while rbx_tune("add_partition_diag") has bit 64):
+ * copies n <= 16 counters to host `out` and zeroes them. */
+int rbx_bench_add_stamps(rbx_ctx *ctx, unsigned long long *out, uint32_t n);
 /* Stream-read roofline probe: reads `bytes` (16-byte aligned buffer) with 16-byte loads. */
 int rbx_bench_stream_read(rbx_ctx *ctx, const void *d_buf, uint64_t bytes, void *d_sink, void *stream);
 /* Stream-write roofline probe: writes `bytes` (16-byte aligned buffer) with 16-byte nontemporal
@@ -44,7 +48,12 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *                           bitmap >= 8 MiB and >= max(2^17, bits / 2^12) keys)
  *   "add_records"           how the partitioned add reports new keys: 0 owner bits, 1 non-owner
  *                           counters, 3 owner records, 2 (default) chosen from the sampled fill
- *   "add_partition_diag"    0 (default) or 4 (diagnostics)
+ *   "add_partition_diag"    0 (default); bits 4|8|16 (diagnostics, wrong answers); 64 (exact:
+ *                           region-pass phase times, read by rbx_bench_add_stamps)
+ *   "add_region_kernel"     partitioned add region pass: 2 (default: 6-byte region pairs,
+ *                           pipelined k_ba_region6), 1 (8-byte pairs, k_ba_region)
+ *   "add_rec_lds_limit"     owner records a region block stages in LDS, 0..7168 (default 7168;
+ *                           tests use small limits to run the direct-report fallback)
  *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,
  *                           2 auto (default: the call's bitmaps exceed 64 MiB)
  *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44

@@ -175,6 +175,7 @@ SIGNATURES = {
     "rbx_enable_peer_access": (C.c_int, [C.c_int, C.c_int]),
     "rbx_bench_slice_probe": (C.c_int, [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint, vp, vp]),
     "rbx_bench_stream_read": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
+    "rbx_bench_add_stamps": (C.c_int, [vp, vp, C.c_uint32]),
     "rbx_bench_stream_write": (C.c_int, [vp, vp, C.c_uint64, vp]),
     "rbx_bench_gather_segments": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp]),
     # binary names (rbx_name)

@@ -154,6 +154,27 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
 // so that the blocks running at one time read different parents.
 constexpr uint32_t kBaRbThreads = 1024, kBaRbTile = 16 * kBaRbThreads;  // 128 KiB image: one block per CU
 
+// Region pairs are 6 bytes when P6 (the default): lo = region offset (16 bits) << 16 | key bits
+// 0-15, hi (u16) = key bits 16-25 (chunks hold <= 2^26 keys), two arrays of cap_out entries per
+// region.  Against 8-byte pairs: a quarter fewer bytes written here and read by the region pass,
+// and 12 registers per thread for a region block's 8 pairs instead of 16.
+template <bool P6>
+__device__ __forceinline__ void ba_put_region(unsigned long long e, uint64_t reg, uint64_t slot,
+                                              unsigned long long *pout, uint64_t cap_out) {
+    if constexpr (P6) {
+        // region reg's bytes: [cap_out lo words][cap_out hi halves] (cap_out is a multiple of 64, so
+        // both rows start 128-byte aligned)
+        uint32_t *lo = (uint32_t *)pout + reg * (cap_out * 3 / 2);
+        uint16_t *hi = (uint16_t *)(lo + cap_out);
+        const uint32_t idx = (uint32_t)(e >> 32), key = (uint32_t)e;
+        ba_run_store((idx << 16) | (key & 0xffffu), lo + slot);
+        ba_run_store((uint16_t)(key >> 16), hi + slot);
+    } else {
+        ba_run_store(e, pout + reg * cap_out + slot);
+    }
+}
+
+template <bool P6>
 __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned long long *__restrict__ pin,
                                                      const uint32_t *__restrict__ cnt_in, uint64_t cap_in,
                                                      uint32_t nparents, uint32_t sub_div, uint32_t items_per_part,
@@ -218,7 +239,7 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
         for (uint32_t i = threadIdx.x; i < m; i += NT) {
             const uint32_t f = s_bkt[i];
             const uint64_t gp = (uint64_t)s_gb[f] + (i - s_start[f]);
-            if (gp < cap_out) ba_run_store(s_img[i], pout + (uint64_t)((parent << fo) + f) * cap_out + gp);
+            if (gp < cap_out) ba_put_region<P6>(s_img[i], (parent << fo) + f, gp, pout, cap_out);
             else *overflow = 1u;
         }
         __syncthreads();
@@ -275,11 +296,14 @@ __device__ __forceinline__ uint32_t ba_slot(uint32_t off, uint32_t t) {
     return ((off * 2654435761u) >> (32 - kBaTableBits)) + t & ((1u << kBaTableBits) - 1);
 }
 
+template <bool STAMP>
 __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ba_region(
     const unsigned long long *__restrict__ p3, const uint32_t *__restrict__ cnt3, uint64_t cap3, uint32_t nregions,
     uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t *__restrict__ new_bits, uint32_t *__restrict__ ctr,
     uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt, uint64_t cap_rec, uint32_t nranges,
-    const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t diag) {
+    const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t diag,
+    unsigned long long *__restrict__ stamps) {
+    PhaseStamps<STAMP> ps;
     constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, T = 1u << kBaTableBits;
     constexpr uint32_t kOff = (1u << kBaRegionBits) - 1;
     constexpr uint32_t NV = kBaRegionWords / 4;  // 16-byte vectors of the region
@@ -296,6 +320,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long e[PER];
     bool loaded = false;
+    ps.start();
     for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
         const uint32_t n = (uint32_t)min<uint64_t>(cnt3[r], cap3);
         if (n == 0) continue;  // uniform
@@ -331,6 +356,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
         }
         if (threadIdx.x < 64) s_rc[threadIdx.x] = 0;
         __syncthreads();
+        ps.mark(0);
         // pass 1: which pairs meet a 0 bit, and which of those bits are met more than once
         uint32_t zm = 0;
 #pragma unroll
@@ -342,6 +368,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             }
         }
         __syncthreads();
+        ps.mark(3);
         // pass 2: a bit met once is owned by its pair; bits met again go through the table
         uint32_t own = 0, pend = 0;
 #pragma unroll
@@ -352,6 +379,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
                 else own |= 1u << p;
             }
         }
+        ps.mark(4);
         bool first = true;
         while (__syncthreads_or(pend != 0u)) {  // uniform; also orders the previous round's reads
             if (!first) {
@@ -390,6 +418,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             }
             pend &= ~ins;  // bits not inserted this round (table full) retry with a cleared table
         }
+        ps.mark(5);
         // owners set their bits; the other kind is reported to the key pass
 #pragma unroll
         for (uint32_t p = 0; p < PER; ++p) {
@@ -403,7 +432,9 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
                 atomicAdd(&ctr[key >> 2], 1u << (8 * (key & 3)));  // no return: not waited on here
             }
         }
-        if (!__syncthreads_or(own != 0u)) continue;  // uniform: no bit changed
+        const bool changed = __syncthreads_or(own != 0u);
+        ps.mark(6);
+        if (!changed) continue;  // uniform: no bit changed
         if (has_words) ((u32x4 *)(bm + w0))[threadIdx.x] = ((const u32x4 *)s_bm)[threadIdx.x];
         if (records && !(diag & 4)) {  // uniform: owner key ids as runs per 2^20-key range
             uint32_t gb = 0;
@@ -429,7 +460,350 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             }
         }
         __syncthreads();  // s_bm / s_rec reuse
+        ps.mark(7);
     }
+    ps.flush(stamps);
+}
+
+// C (6-byte pairs, pipelined) -----------------------------------------------------------
+// The same resolution as k_ba_region, with the next region's inputs in flight while the current
+// one is resolved.  k_ba_region waited, per region, for its pair count, then for the region's pairs
+// and bitmap (two dependent memory round trips before any work), and took 60 B/lane of spills.
+// Here, right after a region's pairs are copied from LDS into registers, the block issues the next
+// region's pairs straight into that LDS buffer (global_load_lds: no registers held for them) and
+// its bitmap into 4 registers, so both land during the current region's passes.
+// An LDS-DMA is a pending LDS write on the VM counter, and a __syncthreads() fence waits for every
+// VM operation, which would drain the prefetch at the first barrier; so the barriers in the body
+// are raw s_barrier with an LDS-counter wait only (ba_bar), the block-wide ORs go through LDS flag
+// words (ba_bar_or), and the one drain is an explicit vmcnt(0) at the top of the next region.
+// LDS (77 KiB: two blocks per CU): the pair buffer (32 KiB lo + 16 KiB hi), the region's bitmap,
+// the met-once / met-again bitsets (8 KiB each), a 512-slot collision table; the owner records
+// reuse the bitmap/bitset/table space (7168 slots) once the bitmap has been written back, and a
+// region with more owners than that (only adversarial batches in records mode) reports them by
+// direct atomics instead.
+__device__ __forceinline__ void ba_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Makes the pair registers opaque at a phase boundary, so the compiler recomputes each pair's word
+// offset, bit and key (a few VALU ops) instead of keeping them live across the phases: at 64 VGPRs
+// that CSE spilled, and a scratch reload waits on the VM counter, which drains the prefetch.
+// LDS atomics of the region passes as inline asm: hipcc waits for every outstanding LDS-DMA
+// (vmcnt(0)) before an LDS atomic it emits itself, even into another LDS object, which drained the
+// prefetch at pass 1.  The asm forms are counted on lgkmcnt like the compiler's own (extra younger
+// LDS operations only make its counted waits stricter); a returning form waits for its result.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ uint32_t lds_or_rtn(uint32_t *p, uint32_t v) {
+    uint32_t r;
+    asm volatile("ds_or_rtn_b32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr(p)), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_or(uint32_t *p, uint32_t v) {
+    asm volatile("ds_or_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add(uint32_t *p, uint32_t v) {
+    asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t *p, uint32_t v) {
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr(p)), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_min(uint32_t *p, uint32_t v) {
+    asm volatile("ds_min_u32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+template <int N> __device__ __forceinline__ void ba_opaque(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+// Bits met again get compact slots instead of a hashed table: after pass 1 every word of the
+// met-again bitset gets the rank base of its bits (one LDS counter add per nonzero word), so a bit's
+// slot is base[word] + the popcount of the met-again bits below it in its word, and its first
+// setter is one atomicMin there -- no claim, no probing.  kBa6Slots slots per round; a region with
+// more bits met again (C2: ~200) takes further rounds.
+constexpr uint32_t kBa6Slots = 1024;
+constexpr uint32_t kBa6Main = 3 * kBaRegionWords + kBa6Slots;  // 7168 words
+static_assert(kBa6Main >= 7168, "record space");
+
+template <bool STAMP>
+__global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ba_region6(
+    const uint32_t *__restrict__ p3, const uint32_t *__restrict__ cnt3, uint64_t cap3, uint32_t nregions,
+    uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t *__restrict__ new_bits, uint32_t *__restrict__ ctr,
+    uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt, uint64_t cap_rec, uint32_t nranges,
+    const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t rec_limit, uint32_t diag,
+    unsigned long long *__restrict__ stamps) {
+    constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, C = kBa6Slots;
+    PhaseStamps<STAMP> ps;
+    constexpr uint32_t kOff = (1u << kBaRegionBits) - 1;
+    constexpr uint32_t NV = kBaRegionWords / 4;  // 16-byte vectors of the region's bitmap
+    static_assert(PER == 8 && NV <= NT, "8 pairs per thread: two lo vectors and one hi vector");
+    // The DMA target is an LDS object of its own, so the compiler can tell that the passes' LDS
+    // accesses (the other object) do not alias it and need not wait for the DMA.
+    __shared__ __attribute__((aligned(16))) uint32_t lds_pairs[kBaMaxRegionPairs * 3 / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kBa6Main + 4 * 64 + 8];
+    uint32_t *s_plo = lds_pairs;                                    // [8192] pair lo words
+    uint16_t *s_phi = (uint16_t *)(lds_pairs + kBaMaxRegionPairs);  // [8192] pair hi halves
+    uint32_t *s_main = lds;
+    uint32_t *s_bm = s_main, *s_seen = s_bm + kBaRegionWords, *s_multi = s_seen + kBaRegionWords;
+    uint32_t *s_tmin = s_multi + kBaRegionWords;                    // [C] first setter per slot
+    uint16_t *s_base = (uint16_t *)s_seen;                          // [2048] slot bases, after pass 1
+    uint32_t *s_rec = s_main;                                       // [kBa6Main] after the write-back
+    uint32_t *s_rc = s_main + kBa6Main, *s_rst = s_rc + 64, *s_rpos = s_rst + 64, *s_rgb = s_rpos + 64;
+    uint32_t *s_flag = s_rgb + 64;  // [0..2] ba_bar_or flags, [6] owner total, [7] bits met again
+    if (*overflow) return;
+    const uint32_t md = *mode;
+    const bool counters = md == 1, records = md == 2, bits = md == 0;
+    const uint32_t rlim = min(rec_limit, kBa6Main);
+    // block-wide OR: call c sets flag c % 3 and clears flag (c + 1) % 3, which the previous reads
+    // of it (call c - 2) finished before call c - 1's barrier
+    uint32_t nor = 0;
+    auto ba_bar_or = [&](uint32_t tid, bool p) -> bool {
+        if (tid == 0) s_flag[(nor + 1) % 3] = 0u;
+        if (__ballot(p) != 0ULL && (tid & 63) == 0) s_flag[nor % 3] = 1u;
+        ba_bar();
+        const bool r = s_flag[nor % 3] != 0u;
+        ++nor;
+        return r;
+    };
+    if (threadIdx.x < 3) s_flag[threadIdx.x] = 0u;
+    // The block's regions are blockIdx.x + i * gridDim.x; lane l of every wave holds the pair count
+    // of region i = ibase + l (one vector load per 64 regions instead of a dependent scalar load per
+    // region).  Returns the first region at or after index i with pairs (uniform), or nregions.
+    uint32_t ibase = 0, cvec = 0;
+    auto load_counts = [&](uint32_t ib) {
+        ibase = ib;
+        const uint32_t rr = blockIdx.x + (ib + (threadIdx.x & 63)) * gridDim.x;
+        cvec = rr < nregions ? (uint32_t)min<uint64_t>(cnt3[rr], cap3) : 0u;
+    };
+    auto next_region = [&](uint32_t i, uint32_t &cnt) -> uint32_t {
+        for (;;) {
+            if (blockIdx.x + ibase * gridDim.x >= nregions) return nregions;
+            if (i >= ibase + 64) {
+                load_counts(i & ~63u);
+                continue;
+            }
+            const uint64_t m = __ballot(cvec != 0u && (threadIdx.x & 63) >= i - ibase);
+            if (m) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                cnt = (uint32_t)__builtin_amdgcn_readlane((int)cvec, (int)l);
+                return blockIdx.x + (ibase + l) * gridDim.x;
+            }
+            i = ibase + 64;
+        }
+    };
+    // the region's pairs -> the LDS buffer (16 B per lane, lane-linear per wave), its bitmap -> registers
+    auto prefetch = [&](uint32_t tid, uint32_t r, uint32_t cnt, u32x4 &bw) {
+        const uint32_t wave = tid >> 6;
+        const uint32_t *lo = p3 + (uint64_t)r * (cap3 * 3 / 2);
+        const uint32_t nlo = (cnt + 3) / 4, nhi = (cnt + 7) / 8;
+#pragma unroll
+        for (uint32_t i = 0; i < 2; ++i) {
+            const uint32_t j = i * NT + tid;
+            if (j < nlo)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)((const u32x4 *)lo + j),
+                                                 (__attribute__((address_space(3))) void *)((u32x4 *)s_plo + i * NT + wave * 64),
+                                                 16, 0, 0);
+        }
+        if (tid < nhi)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)((const u32x4 *)(lo + cap3) + tid),
+                                             (__attribute__((address_space(3))) void *)((u32x4 *)s_phi + wave * 64),
+                                             16, 0, 0);
+        const uint64_t w0 = (uint64_t)r * kBaRegionWords;
+        bw = u32x4{0u, 0u, 0u, 0u};
+        if (tid < NV && w0 + 4 * tid < nwords4) bw = ((const u32x4 *)(bm + w0))[tid];
+    };
+    uint32_t n = 0;
+    load_counts(0);
+    uint32_t r = next_region(0, n);
+    u32x4 bw;
+    if (r < nregions) prefetch(threadIdx.x, r, n, bw);
+    ps.start();
+    while (r < nregions) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this region's pairs and bitmap
+        ba_bar();
+        ps.mark(0);
+        // the thread index made opaque per region: values derived from it (LDS addresses, lane
+        // predicates) are recomputed instead of hoisted out of the loop and kept live (spilled)
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        // re-derived at each phase, so no copy of it lives (and spills) across the phases
+        auto fresh_tid = [&]() {
+            tid = threadIdx.x;
+            asm volatile("" : "+v"(tid));
+        };
+        // my pairs: q = p * NT + tid (strided, so every thread holds ceil(n / NT) or one fewer: with
+        // 8 consecutive pairs per thread a 5.3K-pair region left a third of the block idle and the
+        // rest on an 8-deep serial chain of LDS round trips)
+        uint32_t lo[PER], hw[PER / 2];
+#pragma unroll
+        for (uint32_t p = 0; p < PER; ++p) lo[p] = s_plo[p * NT + tid];
+#pragma unroll
+        for (uint32_t p = 0; p < PER; p += 2)
+            hw[p / 2] = (uint32_t)s_phi[p * NT + tid] | (uint32_t)s_phi[(p + 1) * NT + tid] << 16;
+        auto valid = [&](uint32_t p) { return p * NT + tid < n; };
+        const uint64_t w0 = (uint64_t)r * kBaRegionWords;
+        const bool has_words = tid < NV && w0 + 4 * tid < nwords4;
+        if (tid < NV) {
+            ((u32x4 *)s_bm)[tid] = bw;
+            ((u32x4 *)s_seen)[tid] = u32x4{0u, 0u, 0u, 0u};
+            ((u32x4 *)s_multi)[tid] = u32x4{0u, 0u, 0u, 0u};
+        }
+        for (uint32_t i = tid; i < C; i += NT) s_tmin[i] = ~0u;
+        if (tid < 64) s_rc[tid] = 0;
+        if (tid == 0) {  // owner total and slot counter (the previous region's reads ended at its last barrier)
+            s_flag[6] = 0u;
+            s_flag[7] = 0u;
+        }
+        ba_bar();  // the pair buffer has been read by every thread: refill it for the next region
+        ps.mark(1);
+        uint32_t nn = 0;
+        const uint32_t rn = next_region((r - blockIdx.x) / gridDim.x + 1, nn);
+        if (rn < nregions && !(diag & 8)) prefetch(tid, rn, nn, bw);
+        ps.mark(2);
+        auto key_of = [&](uint32_t p) { return ((hw[p >> 1] >> (16 * (p & 1))) & 0xffffu) << 16 | (lo[p] & 0xffffu); };
+        // pass 1: which pairs meet a 0 bit, and which of those bits are met more than once
+        uint32_t zm = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < PER; ++p) {
+            const uint32_t off = lo[p] >> 16, w = off >> 5, b = bit_in_word(off);
+            if (valid(p) && (s_bm[w] & b) == 0u) {
+                zm |= 1u << p;
+                if (lds_or_rtn(&s_seen[w], b) & b) lds_or(&s_multi[w], b);
+            }
+        }
+        ba_bar();
+        ps.mark(3);
+        ba_opaque(lo);
+        fresh_tid();
+        // pass 2: a bit met once is owned by its pair; bits met again get slots (see kBa6Slots)
+        uint32_t own = 0, pend = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < PER; ++p) {
+            if (zm & (1u << p)) {
+                const uint32_t off = lo[p] >> 16;
+                if (s_multi[off >> 5] & bit_in_word(off)) pend |= 1u << p;
+                else own |= 1u << p;
+            }
+        }
+        {  // slot bases of my two met-again words (s_seen, now s_base, is dead after pass 1)
+            const uint32_t m0 = s_multi[2 * tid], m1 = s_multi[2 * tid + 1];
+            const uint32_t c = __popc(m0) + __popc(m1);
+            if (c) {
+                const uint32_t b0 = lds_add_rtn(&s_flag[7], c);
+                s_base[2 * tid] = (uint16_t)b0;
+                s_base[2 * tid + 1] = (uint16_t)(b0 + __popc(m0));
+            }
+        }
+        ba_bar();
+        ps.mark(4);
+        const uint32_t nmulti = s_flag[7];  // uniform
+        ba_opaque(lo);
+        fresh_tid();
+        auto slot_of = [&](uint32_t p) {
+            const uint32_t off = lo[p] >> 16, w = off >> 5, b = bit_in_word(off);
+            return (uint32_t)s_base[w] + (uint32_t)__popc(s_multi[w] & (b - 1u));
+        };
+        for (uint32_t r0 = 0; r0 < nmulti; r0 += C) {  // uniform; one round at C2
+            ba_opaque(lo);
+            ba_opaque(hw);
+            fresh_tid();
+            if (r0) {
+                ba_bar();  // the previous round's reads of s_tmin
+                for (uint32_t i = tid; i < C; i += NT) s_tmin[i] = ~0u;
+                ba_bar();
+            }
+#pragma unroll
+            for (uint32_t p = 0; p < PER; ++p) {
+                if (pend & (1u << p)) {
+                    const uint32_t sl = slot_of(p) - r0;
+                    if (sl < C) lds_min(&s_tmin[sl], key_of(p));
+                }
+            }
+            ba_bar();
+            ba_opaque(lo);
+            ba_opaque(hw);
+            fresh_tid();
+#pragma unroll
+            for (uint32_t p = 0; p < PER; ++p) {
+                if (pend & (1u << p)) {
+                    const uint32_t sl = slot_of(p) - r0;
+                    if (sl < C && s_tmin[sl] == key_of(p)) own |= 1u << p;
+                }
+            }
+        }
+        ps.mark(5);
+        // owners set their bits; the other kind is reported to the key pass
+        ba_opaque(lo);
+        ba_opaque(hw);
+        fresh_tid();
+#pragma unroll
+        for (uint32_t p = 0; p < PER; ++p) {
+            const uint32_t off = lo[p] >> 16;
+            if (own & (1u << p)) {
+                lds_or(&s_bm[off >> 5], bit_in_word(off));
+                if (diag & 4) continue;
+                const uint32_t key = key_of(p);
+                if (bits) atomicOr(&new_bits[key >> 5], 1u << (key & 31));
+                else if (records) lds_add(&s_rc[key >> kBaKeyRangeBits], 1u);
+            } else if (counters && !(diag & 4) && valid(p)) {
+                const uint32_t key = key_of(p);
+                atomicAdd(&ctr[key >> 2], 1u << (8 * (key & 3)));  // no return: not waited on here
+            }
+        }
+        fresh_tid();
+        const uint32_t lane = tid & 63, wave = tid >> 6;
+        if (records) {  // owner total of the block (one LDS atomic per wave)
+            uint32_t c = __popc(own);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            if (lane == 0 && c) lds_add(&s_flag[6], c);
+        }
+        const bool changed = ba_bar_or(tid, own != 0u);
+        ps.mark(6);
+        if (changed) {  // uniform
+            if (has_words) ((u32x4 *)(bm + w0))[tid] = ((const u32x4 *)s_bm)[tid];
+            if (records && !(diag & 4)) {
+                const uint32_t tot = s_flag[6];
+                if (tot > rlim) {  // uniform: too many records for LDS, report them directly
+#pragma unroll
+                    for (uint32_t p = 0; p < PER; ++p) {
+                        if (own & (1u << p)) {
+                            const uint32_t key = key_of(p);
+                            atomicOr(&new_bits[key >> 5], 1u << (key & 31));
+                        }
+                    }
+                } else {  // owner key ids as runs per 2^20-key range
+                    uint32_t gb = 0;
+                    const uint32_t q = tid - 128;
+                    const bool reserver = tid >= 128 && q < nranges;
+                    if (tid < 64) bk_scan128(s_rc, nranges, s_rst, s_rpos, lane);
+                    else if (reserver && s_rc[q]) gb = atomicAdd(&rec_cnt[q], s_rc[q]);
+                    ba_bar();  // the scan, and the write-back's reads of s_bm, before s_rec is written
+#pragma unroll
+                    for (uint32_t p = 0; p < PER; ++p) {
+                        if (own & (1u << p)) {
+                            const uint32_t key = key_of(p);
+                            s_rec[atomicAdd(&s_rpos[key >> kBaKeyRangeBits], 1u)] = key;
+                        }
+                    }
+                    if (reserver) s_rgb[q] = gb;
+                    ba_bar();
+                    // records per range <= 2^20 keys x k = cap_rec: no overflow
+                    for (uint32_t rq = wave; rq < nranges; rq += NT / 64) {
+                        const uint32_t rn2 = s_rc[rq], st = s_rst[rq];
+                        uint32_t *dst = recs + (uint64_t)rq * cap_rec + s_rgb[rq];
+                        for (uint32_t t = lane; t < rn2; t += 64) run_store(s_rec[st + t], dst + t);
+                    }
+                }
+            }
+        }
+        ba_bar();  // s_bm / s_rec / s_rc / s_flag[6] reuse
+        ps.mark(7);
+        r = rn;
+        n = nn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ps.flush(stamps);
 }
 
 // D ------------------------------------------------------------------------------------
@@ -536,6 +910,14 @@ __global__ __launch_bounds__(256) void k_ba_final(const uint32_t *__restrict__ n
 // EXPERIMENTS (rbx_tune "add_region_grid"): k_ba_region blocks; each walks regions r, r + grid, ...
 static uint32_t g_region_grid = 2048;
 void set_add_region_grid(int v) { g_region_grid = (uint32_t)v; }
+// EXPERIMENTS (rbx_tune "add_region_kernel"): 2 (default) 6-byte region pairs + the pipelined
+// k_ba_region6; 1 the r02 8-byte pairs + k_ba_region (A/B only)
+static int g_region_kernel = 2;
+void set_add_region_kernel(int v) { g_region_kernel = v; }
+// rbx_tune "add_rec_lds_limit" (tests): owner records a k_ba_region6 block stages in LDS before it
+// reports a region's owners by direct atomics instead (default and maximum kBa6Main)
+static uint32_t g_rec_limit = kBa6Main;
+void set_add_rec_lds_limit(int v) { g_rec_limit = (uint32_t)v; }
 
 template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
@@ -546,11 +928,30 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)), dim3(kBaS1Threads), 0, st,
                        a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1, a.overflow);
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
-    hipLaunchKernelGGL(k_ba_rebucket, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub, it1, a.s3,
-                       a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
-    hipLaunchKernelGGL(k_ba_region, dim3(std::min<uint32_t>(a.nregions, g_region_grid)), dim3(kBaRegionThreads), 0, st, a.p3,
-                       a.cnt3, a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
-                       a.nranges, a.overflow, a.mode, a.diag);
+    const dim3 rgrid(std::min<uint32_t>(a.nregions, g_region_grid));
+    if (g_region_kernel == 1) {
+        hipLaunchKernelGGL(k_ba_rebucket<false>, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub,
+                           it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
+        if (a.stamps)
+            hipLaunchKernelGGL(k_ba_region<true>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,
+                               a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
+                               a.mode, a.diag, a.stamps);
+        else
+            hipLaunchKernelGGL(k_ba_region<false>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,
+                               a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
+                               a.mode, a.diag, a.stamps);
+    } else {
+        hipLaunchKernelGGL(k_ba_rebucket<true>, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub,
+                           it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
+        if (a.stamps)
+            hipLaunchKernelGGL(k_ba_region6<true>, rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3,
+                               a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
+                               a.nranges, a.overflow, a.mode, g_rec_limit, a.diag, a.stamps);
+        else
+            hipLaunchKernelGGL(k_ba_region6<false>, rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3,
+                               a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
+                               a.nranges, a.overflow, a.mode, g_rec_limit, a.diag, a.stamps);
+    }
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
     // one thread per new_bits word (32 keys): the per-thread chain of a smaller grid was the C1 add's third-largest cost

@@ -38,8 +38,8 @@ __device__ __forceinline__ void bk_hash(const KeysDev &keys, uint64_t i, uint64_
 }
 
 // exclusive scan of cnt[0..nb) (nb <= 128) by wave 0 into start[] and pos[]
-__device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos) {
-    const uint32_t lane = threadIdx.x;
+__device__ __forceinline__ void bk_scan128(const uint32_t *cnt, uint32_t nb, uint32_t *start, uint32_t *pos,
+                                           uint32_t lane = threadIdx.x) {
     const uint32_t a = 2 * lane < nb ? cnt[2 * lane] : 0u;
     const uint32_t b = 2 * lane + 1 < nb ? cnt[2 * lane + 1] : 0u;
     uint32_t x = a + b;
@@ -126,5 +126,27 @@ __device__ __forceinline__ void bk_scan256(const uint32_t *cnt, uint32_t nb, uin
         ex += v[j];
     }
 }
+
+// Phase timer for A/B diagnostics (template-gated: the production instantiation carries none of
+// it): s_memtime deltas of the block's wave 0 summed per phase, added by thread 0 to dst[0..N).
+template <bool ON, int N = 8> struct PhaseStamps {
+    uint64_t t = 0, acc[N] = {};
+    __device__ __forceinline__ void start() {
+        if constexpr (ON) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void mark(int i) {
+        if constexpr (ON) {
+            const uint64_t n = __builtin_amdgcn_s_memtime();
+            acc[i] += n - t;
+            t = n;
+        }
+    }
+    __device__ __forceinline__ void flush(unsigned long long *dst) {
+        if constexpr (ON) {
+            if (threadIdx.x == 0)
+                for (int i = 0; i < N; ++i) atomicAdd(dst + i, (unsigned long long)acc[i]);
+        }
+    }
+};
 
 }  // namespace rbx

@@ -179,6 +179,7 @@ struct rbx_ctx {
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
+    DevBuf pa_stamps;  // add_partition_diag & 64: region-pass phase times (rbx_bench_add_stamps)
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     // all-zero words standing in for a missing bitmap in multi-tenant contains (GETBIT on a
     // missing key reads 0; the key is not created), grown on demand, never written by a kernel
@@ -592,6 +593,13 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         a.out_new = d_out_new;
         a.count = d_count;
         a.diag = (uint32_t)g_add_partition_diag;
+        if (a.diag & 64) {
+            if (c->pa_stamps.cap == 0) {
+                RBX_TRY(c->pa_stamps.reserve(16 * 8));
+                HIP_TRY(hipMemsetAsync(c->pa_stamps.p, 0, 16 * 8, st));
+            }
+            a.stamps = c->pa_stamps.as<unsigned long long>();
+        }
         HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
         HIP_TRY(hipMemsetAsync(a.new_bits, 0, (uint64_t)a.nranges << (kBaKeyRangeBits - 5) << 2, st));
         launch_add_partitioned_chunk(a, fl, st);
@@ -2546,6 +2554,18 @@ int rbx_bench_slice_probe(rbx_ctx *c, const void *d_entries, uint64_t per_bucket
     return RBX_OK;
 }
 
+int rbx_bench_add_stamps(rbx_ctx *c, unsigned long long *out, uint32_t n) {
+    if (!c || !out || n > 16) return fail(RBX_E_ILLEGAL_ARGUMENT, "rbx_bench_add_stamps: n <= 16");
+    if (c->pa_stamps.cap == 0) {
+        memset(out, 0, n * 8);
+        return RBX_OK;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, c->pa_stamps.p, n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(c->pa_stamps.p, 0, 16 * 8));
+    return RBX_OK;
+}
+
 int rbx_bench_stream_read(rbx_ctx *c, const void *d_buf, uint64_t bytes, void *d_sink, void *stream) {
     if (!c || !d_buf || !d_sink || ((uintptr_t)d_buf & 15)) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
     RBX_TRY(set_device(c));
@@ -2842,7 +2862,7 @@ int rbx_tune(const char *key, int value) {
     // emits no records, 8 = it loads only its first two regions' pairs (compute floor), 16 = it
     // only loads (load floor).  0 = normal.
     if (!strcmp(key, "add_partition_diag")) {
-        if (value < 0 || (value & ~28) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag: bits of 4|8|16");
+        if (value < 0 || (value & ~92) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag: bits of 4|8|16|64");
         g_add_partition_diag = value;
         return RBX_OK;
     }
@@ -2899,6 +2919,16 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_region_grid")) {
         if (value < 256 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_grid in [256, 65536]");
         set_add_region_grid(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_region_kernel")) {
+        if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_kernel in {1, 2}");
+        set_add_region_kernel(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_rec_lds_limit")) {
+        if (value < 0 || value > 7168) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rec_lds_limit in [0, 7168]");
+        set_add_rec_lds_limit(value);
         return RBX_OK;
     }
     if (!strcmp(key, "contains_emit2_nt")) {

@@ -96,6 +96,8 @@ void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream
 void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
 void set_contains_stage1_per(int v);  // 1 or 2 (default)
 void set_add_region_grid(int v);  // 256..65536 (default 2048)
+void set_add_region_kernel(int v);  // 1 (r02 8-byte pairs) or 2 (default: 6-byte pairs, pipelined)
+void set_add_rec_lds_limit(int v);  // 0..7168 (tests)
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 // Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB
@@ -126,6 +128,7 @@ struct BaArgs {
     uint8_t *out_new;
     unsigned long long *count;
     uint32_t diag;                // diagnostics only (rbx_tune "add_partition_diag"); 0 in normal operation
+    unsigned long long *stamps;   // diagnostics only (add_partition_diag & 64): region-pass phase times, else null
 };
 void launch_add_partitioned_chunk(const BaArgs &a, int klen_fast, hipStream_t st);
 

@@ -788,8 +788,8 @@ def test_partitioned_add_parity(client, fresh, mode, records, size, k, L):
 
 @pytest.mark.parametrize("records", [0, 1, 3])
 def test_partitioned_add_collision_table_rounds(client, fresh, records):
-    """Every key twice in one 2^16-bit region: ~3000 bits are met by two pairs, three times the
-    region kernel's 1024-slot collision table, so the table is cleared and refilled for further
+    """Every key twice in one 2^16-bit region: ~3000 bits are met by two pairs, about six times the
+    region kernel's 512-slot collision table, so the table is cleared and refilled for further
     rounds.  Flags, count and bitmap equal the oracle's in-order fold."""
     from redisson_amd import _lib as L_
 
@@ -812,6 +812,42 @@ def test_partitioned_add_collision_table_rounds(client, fresh, records):
     assert cg == cr and np.array_equal(ng, nr)
     assert cg2 == cr2 and np.array_equal(ng2, nr2)
     assert f.exportBitmap() == ref.redis_string()
+    f.delete()
+
+
+@pytest.mark.parametrize("tune", [(b"add_rec_lds_limit", 0), (b"add_rec_lds_limit", 64), (b"add_region_kernel", 1)])
+@pytest.mark.parametrize("records", [1, 3])
+def test_partitioned_add_region_variants(client, fresh, tune, records):
+    """The region pass's other branches give the oracle's answers too: owner records past the
+    block's LDS record space (add_rec_lds_limit 0 / 64: every region, or most, reports its owners by
+    direct atomics instead of record runs), and the r02 kernel on 8-byte region pairs
+    (add_region_kernel 1).  Two batches, the second re-adding and repeating keys; flags, counts,
+    bitmap bytes and count() equal the in-order SETBIT fold."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(4242 + records)
+    n = 300_000
+    mat = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    second = np.concatenate([mat[n // 8: n // 2], mat[rng.integers(0, n // 2, size=n // 4)], mat[n // 2:]])
+    f = client.getBloomFilter(fresh)
+    f.tryInitRaw(1 << 28, 7)
+    ref = O.OracleBloom(1 << 28, 7)
+    key, val = tune
+    assert L_.lib().rbx_tune(b"add_partition", 1) == 0
+    assert L_.lib().rbx_tune(b"add_records", records) == 0
+    assert L_.lib().rbx_tune(key, val) == 0
+    try:
+        for batch in (mat[: n // 4], second):
+            cg, ng = f.addEach(Arena.fixed(batch))
+            cr, nr = ref.add(*O.fixed_arena(batch), per_key=True)
+            assert cg == cr and np.array_equal(ng, nr)
+    finally:
+        L_.lib().rbx_tune(b"add_partition", 2)
+        L_.lib().rbx_tune(b"add_records", 2)
+        L_.lib().rbx_tune(b"add_rec_lds_limit", 7168)
+        L_.lib().rbx_tune(b"add_region_kernel", 2)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.count() == ref.count()
     f.delete()
 
 

@@ -230,6 +230,35 @@ def main():
         for dg, v in res.items():
             print(json.dumps({"bench": "add_partition_diag", "diag": dg, "ms_median": statistics.median(v)}), flush=True)
 
+    if "regstamp" in a.what:
+        # region-pass phase times (add_partition_diag 64, exact results) of each region kernel,
+        # C2 add of n/2 keys into an empty 2^32-bit filter; summed over blocks, in ms of one CU's
+        # wave 0 (s_memtime ticks at 100 MHz) per block slot
+        import ctypes as C
+
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        names = ["top_wait", "setup", "prefetch", "pass1", "pass2", "table", "owners", "writeback"]
+        for rk in (1, 2, 1, 2):
+            assert L.lib().rbx_tune(b"add_region_kernel", rk) == 0
+            assert L.lib().rbx_tune(b"add_partition_diag", 64) == 0
+            fb = client.getBloomFilter(f"rs-{rk}")
+            fb.tryInitRaw(1 << 32, 7)
+            h = BloomHandle(client, f"rs-{rk}")
+            buf = (C.c_ulonglong * 16)()
+            L.lib().rbx_bench_add_stamps(client.ctx, buf, 16)  # clear
+            cnt.zero_()
+            ms = timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(), stream=sp), 1)
+            assert L.lib().rbx_bench_add_stamps(client.ctx, buf, 16) == 0
+            tot = sum(buf[:8])
+            print(json.dumps({"bench": "regstamp", "region_kernel": rk, "add_ms": ms, "new": int(cnt[0].item()),
+                              "share": {nm: buf[i] / tot for i, nm in enumerate(names)},
+                              "ticks_per_block_slot": tot / 512}), flush=True)
+            h.close()
+            fb.delete()
+        L.lib().rbx_tune(b"add_partition_diag", 0)
+        L.lib().rbx_tune(b"add_region_kernel", 2)
+
     if "addab" in a.what:
         # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
         # round, fresh filter per run: RBX_ADDAB="key=v,key=v;key=v" ("-" = defaults)
@@ -254,7 +283,8 @@ def main():
                 fb.delete()
                 for kv in filter(None, ("" if v == "-" else v).split(",")):
                     key = kv.split("=")[0]
-                    L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2}.get(key, 0))
+                    L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2, "add_region_kernel": 2,
+                                                       "add_region_grid": 2048, "add_rec_lds_limit": 7168}.get(key, 0))
         assert len(set(news.values())) == 1, news
         for v, t in res.items():
             med = statistics.median(t)
