@@ -175,7 +175,12 @@ def gather_over_ranks(world, v: int) -> list[int]:
 # ------------------------------------------------------------------------------------------
 # measurement helpers
 # ------------------------------------------------------------------------------------------
+C2_PROFILED_KEYS = 100_000_000  # keys per contains call in the PMC profiles of profiles/traffic.json
+
+
 def load_traffic(path, kernel, field="hbm_bytes_per_launch"):
+    if path is None:
+        return None
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -519,9 +524,13 @@ def run_c2(args, world, rank, local):
     algo_bytes = n * (32 + K * 8)  # 32 B key + k x 8 B gathered per key
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
     floor_bytes = n * 32 + SIZE // 8  # what any streaming design must move: the keys and the bitmap once
-    traffic = load_traffic(args.traffic_json, "contains_pipeline", "hbm_bytes_by_class") or \
-        load_traffic(args.traffic_json, "contains_pipeline")
-    reqf = request_fields(args.traffic_json, "contains_pipeline", kern_ms, gathers_per_s, writes_per_s)
+    # profiles/traffic.json holds PMC counts of 100M-key calls (the default workload); a run with
+    # another --keys gets no PMC-derived fields rather than counts of a different call
+    pmc_ok = n == C2_PROFILED_KEYS
+    traffic = (load_traffic(args.traffic_json, "contains_pipeline", "hbm_bytes_by_class") or
+               load_traffic(args.traffic_json, "contains_pipeline")) if pmc_ok else None
+    reqf = request_fields(args.traffic_json if pmc_ok else None, "contains_pipeline", kern_ms, gathers_per_s,
+                          writes_per_s)
     res = {
         "metric": "Bloom contains keys/sec (whole node), C2: one 2^32-bit filter, k=7, 32-byte keys",
         "value": value, "unit": "keys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -531,7 +540,8 @@ def run_c2(args, world, rank, local):
                                "(50% present) vs one 2^32-bit k=7 filter per GPU",
                    "keys_per_gpu": n, "key_bytes": 32, "size_bits": SIZE, "k": K,
                    "parallelism": f"replicas x{world} of one filter (same adds on every rank, bitmap digests "
-                                  f"equal), contains keys split across replicas, no data-path collective"},
+                                  f"equal), each replica serving its own {n / 1e6:g}M-key contains stream "
+                                  "(weak scaling), no data-path collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
@@ -551,15 +561,18 @@ def run_c2(args, world, rank, local):
                      # working set (> 1: early exit and LDS probes avoid most random gathers)
                      "gather_peak_per_s": gathers_per_s, "gather_frac": (n * K / (kern_ms / 1e3)) / gathers_per_s},
         "extra": {"add_keys_per_s_per_gpu": half / (t_add.ms / 1e3), "add_new_keys": n_new,
+                  "pmc_fields": "profiles/traffic.json (100M-key calls)" if pmc_ok else
+                  f"omitted: PMC profiled at {C2_PROFILED_KEYS} keys per call, this run {n}",
                   "replica_digest": f"{digest:016x}", "replicas_identical": len(set(digests)) == 1,
                   "present_per_step": total_present // args.steps, "wall_s_timed": wall,
                   "contains_direct_kernel_ms": direct_ms,
                   "contains_direct_keys_per_s_per_gpu": n / (direct_ms / 1e3),
                   # the setup add = the partitioned add pipeline (add_partitioned.hip), PMC per call
                   "add_ms": t_add.ms,
-                  "add_traffic": load_traffic(args.traffic_json, "add_pipeline", "hbm_bytes_by_class") or
-                  load_traffic(args.traffic_json, "add_pipeline"),
-                  "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch"),
+                  "add_traffic": (load_traffic(args.traffic_json, "add_pipeline", "hbm_bytes_by_class") or
+                                  load_traffic(args.traffic_json, "add_pipeline")) if pmc_ok else None,
+                  "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch")
+                  if pmc_ok else None,
                   "host_path": hostpath,
                   "c2_tryinit_nonpow2": nonpow2},
     }

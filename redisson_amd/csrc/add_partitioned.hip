@@ -174,17 +174,22 @@ __device__ __forceinline__ void ba_put_region(unsigned long long e, uint64_t reg
     }
 }
 
-template <bool P6>
+// 16K-pair tiles, one 1024-thread block per CU (8K-pair tiles at two blocks per CU, each
+// overlapping the other's loads, measured 1.65 -> 1.78 ms).  A slot's bucket is read back from its
+// pair (no bucket byte array).
+template <bool P6, bool STAMP>
 __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned long long *__restrict__ pin,
                                                      const uint32_t *__restrict__ cnt_in, uint64_t cap_in,
                                                      uint32_t nparents, uint32_t sub_div, uint32_t items_per_part,
                                                      uint32_t shift_out, uint32_t fo, uint32_t nparts_out,
                                                      unsigned long long *__restrict__ pout,
                                                      uint32_t *__restrict__ cnt_out, uint64_t cap_out,
-                                                     uint32_t *__restrict__ overflow) {
+                                                     uint32_t *__restrict__ overflow,
+                                                     unsigned long long *__restrict__ stamps) {
     constexpr int NT = kBaRbThreads, PER = 8, TILE = kBaRbTile;  // PER uint4 = two pairs each
+    PhaseStamps<STAMP, 4> ps;
+    ps.start();
     __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
-    __shared__ uint8_t s_bkt[TILE];
     __shared__ uint32_t s_cnt[256], s_start[256], s_pos[256], s_gb[256];
     const uint32_t nf = 1u << fo, fmask = nf - 1;
     const uint32_t nparts = nparents * sub_div;
@@ -215,6 +220,7 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
             if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u);
         }
         __syncthreads();
+        ps.mark(0);
         uint32_t gb = 0;
         if (threadIdx.x < 64) bk_scan256(s_cnt, nf, s_start, s_pos);
         else if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) {
@@ -223,6 +229,7 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
             if (s_cnt[f] && r < nparts_out) gb = atomicAdd(&cnt_out[r], s_cnt[f]);
         }
         __syncthreads();
+        ps.mark(1);
 #pragma unroll
         for (int p = 0; p < 2 * PER; ++p) {
             const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
@@ -230,20 +237,23 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
                 const uint32_t f = (uint32_t)(e[p] >> (32 + shift_out)) & fmask;
                 const uint32_t slot = atomicAdd(&s_pos[f], 1u);
                 s_img[slot] = e[p];
-                s_bkt[slot] = (uint8_t)f;
             }
         }
         // the reservation results reach LDS only now: the placement above overlapped their round trip
         if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) s_gb[threadIdx.x - 256] = gb;
         __syncthreads();
+        ps.mark(2);
         for (uint32_t i = threadIdx.x; i < m; i += NT) {
-            const uint32_t f = s_bkt[i];
+            const unsigned long long e1 = s_img[i];
+            const uint32_t f = (uint32_t)(e1 >> (32 + shift_out)) & fmask;
             const uint64_t gp = (uint64_t)s_gb[f] + (i - s_start[f]);
-            if (gp < cap_out) ba_put_region<P6>(s_img[i], (parent << fo) + f, gp, pout, cap_out);
+            if (gp < cap_out) ba_put_region<P6>(e1, (parent << fo) + f, gp, pout, cap_out);
             else *overflow = 1u;
         }
         __syncthreads();
+        ps.mark(3);
     }
+    ps.flush(stamps);
 }
 
 // mode -----------------------------------------------------------------------------------
@@ -618,9 +628,9 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     u32x4 bw;
     if (r < nregions) prefetch(threadIdx.x, r, n, bw);
     ps.start();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first region's pairs and bitmap
+    ba_bar();
     while (r < nregions) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this region's pairs and bitmap
-        ba_bar();
         ps.mark(0);
         // the thread index made opaque per region: values derived from it (LDS addresses, lane
         // predicates) are recomputed instead of hoisted out of the loop and kept live (spilled)
@@ -758,9 +768,10 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
             for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
             if (lane == 0 && c) lds_add(&s_flag[6], c);
         }
-        const bool changed = ba_bar_or(tid, own != 0u);
+        // the region's words go back whether or not a bit changed (they are this block's alone)
+        ba_bar();
         ps.mark(6);
-        if (changed) {  // uniform
+        {
             if (has_words) ((u32x4 *)(bm + w0))[tid] = ((const u32x4 *)s_bm)[tid];
             if (records && !(diag & 4)) {
                 const uint32_t tot = s_flag[6];
@@ -797,7 +808,10 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
                 }
             }
         }
-        ba_bar();  // s_bm / s_rec / s_rc / s_flag[6] reuse
+        // one barrier ends this region and starts the next: the next region's pairs and bitmap (and
+        // this region's stores) are complete, and s_bm / s_rec / s_rc / s_flag[6] may be reused
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ba_bar();
         ps.mark(7);
         r = rn;
         n = nn;
@@ -929,9 +943,15 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
                        a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1, a.overflow);
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
     const dim3 rgrid(std::min<uint32_t>(a.nregions, g_region_grid));
+    unsigned long long *rst = a.stamps ? a.stamps + 8 : nullptr;
+#define BA_REBUCKET(P6, ST)                                                                                         \
+    hipLaunchKernelGGL((k_ba_rebucket<P6, ST>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, \
+                       kBaSub, it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
+    if (g_region_kernel == 1) BA_REBUCKET(false, false);
+    else if (a.stamps) BA_REBUCKET(true, true);
+    else BA_REBUCKET(true, false);
+#undef BA_REBUCKET
     if (g_region_kernel == 1) {
-        hipLaunchKernelGGL(k_ba_rebucket<false>, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub,
-                           it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
         if (a.stamps)
             hipLaunchKernelGGL(k_ba_region<true>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,
                                a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
@@ -941,16 +961,13 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
                                a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
                                a.mode, a.diag, a.stamps);
     } else {
-        hipLaunchKernelGGL(k_ba_rebucket<true>, dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub,
-                           it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow);
-        if (a.stamps)
-            hipLaunchKernelGGL(k_ba_region6<true>, rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3,
-                               a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
-                               a.nranges, a.overflow, a.mode, g_rec_limit, a.diag, a.stamps);
-        else
-            hipLaunchKernelGGL(k_ba_region6<false>, rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3,
-                               a.cap3, a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec,
-                               a.nranges, a.overflow, a.mode, g_rec_limit, a.diag, a.stamps);
+#define BA_REGION6(ST)                                                                                                    \
+    hipLaunchKernelGGL((k_ba_region6<ST>),    rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3, a.cap3, \
+                       a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges,          \
+                       a.overflow, a.mode, g_rec_limit, a.diag, a.stamps)
+        if (a.stamps) BA_REGION6(true);
+        else BA_REGION6(false);
+#undef BA_REGION6
     }
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);

@@ -820,7 +820,7 @@ def test_partitioned_add_collision_table_rounds(client, fresh, records):
 def test_partitioned_add_region_variants(client, fresh, tune, records):
     """The region pass's other branches give the oracle's answers too: owner records past the
     block's LDS record space (add_rec_lds_limit 0 / 64: every region, or most, reports its owners by
-    direct atomics instead of record runs), and the r02 kernel on 8-byte region pairs
+    direct atomics instead of record runs), the r02 kernel on 8-byte region pairs
     (add_region_kernel 1).  Two batches, the second re-adding and repeating keys; flags, counts,
     bitmap bytes and count() equal the in-order SETBIT fold."""
     from redisson_amd import _lib as L_

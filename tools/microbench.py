@@ -251,9 +251,13 @@ def main():
             ms = timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(), stream=sp), 1)
             assert L.lib().rbx_bench_add_stamps(client.ctx, buf, 16) == 0
             tot = sum(buf[:8])
+            rtot = sum(buf[8:12])
+            rb = ["load_count", "scan_reserve", "place", "store"]
             print(json.dumps({"bench": "regstamp", "region_kernel": rk, "add_ms": ms, "new": int(cnt[0].item()),
                               "share": {nm: buf[i] / tot for i, nm in enumerate(names)},
-                              "ticks_per_block_slot": tot / 512}), flush=True)
+                              "ticks_per_block_slot": tot / 512,
+                              "rebucket_share": {nm: buf[8 + i] / max(rtot, 1) for i, nm in enumerate(rb)},
+                              "rebucket_ticks_per_cu": rtot / 256}), flush=True)
             h.close()
             fb.delete()
         L.lib().rbx_tune(b"add_partition_diag", 0)
