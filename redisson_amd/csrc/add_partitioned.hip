@@ -544,9 +544,8 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     unsigned long long *__restrict__ stamps) {
     constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, C = kBa6Slots;
     PhaseStamps<STAMP> ps;
-    constexpr uint32_t kOff = (1u << kBaRegionBits) - 1;
     constexpr uint32_t NV = kBaRegionWords / 4;  // 16-byte vectors of the region's bitmap
-    static_assert(PER == 8 && NV <= NT, "8 pairs per thread: two lo vectors and one hi vector");
+    static_assert(PER == 8 && NV <= NT, "8 pair slots and at most one 16-byte bitmap vector per thread");
     // The DMA target is an LDS object of its own, so the compiler can tell that the passes' LDS
     // accesses (the other object) do not alias it and need not wait for the DMA.
     __shared__ __attribute__((aligned(16))) uint32_t lds_pairs[kBaMaxRegionPairs * 3 / 2];
@@ -559,23 +558,11 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     uint16_t *s_base = (uint16_t *)s_seen;                          // [2048] slot bases, after pass 1
     uint32_t *s_rec = s_main;                                       // [kBa6Main] after the write-back
     uint32_t *s_rc = s_main + kBa6Main, *s_rst = s_rc + 64, *s_rpos = s_rst + 64, *s_rgb = s_rpos + 64;
-    uint32_t *s_flag = s_rgb + 64;  // [0..2] ba_bar_or flags, [6] owner total, [7] bits met again
+    uint32_t *s_flag = s_rgb + 64;  // [6] owner total, [7] bits met again
     if (*overflow) return;
     const uint32_t md = *mode;
     const bool counters = md == 1, records = md == 2, bits = md == 0;
     const uint32_t rlim = min(rec_limit, kBa6Main);
-    // block-wide OR: call c sets flag c % 3 and clears flag (c + 1) % 3, which the previous reads
-    // of it (call c - 2) finished before call c - 1's barrier
-    uint32_t nor = 0;
-    auto ba_bar_or = [&](uint32_t tid, bool p) -> bool {
-        if (tid == 0) s_flag[(nor + 1) % 3] = 0u;
-        if (__ballot(p) != 0ULL && (tid & 63) == 0) s_flag[nor % 3] = 1u;
-        ba_bar();
-        const bool r = s_flag[nor % 3] != 0u;
-        ++nor;
-        return r;
-    };
-    if (threadIdx.x < 3) s_flag[threadIdx.x] = 0u;
     // The block's regions are blockIdx.x + i * gridDim.x; lane l of every wave holds the pair count
     // of region i = ibase + l (one vector load per 64 regions instead of a dependent scalar load per
     // region).  Returns the first region at or after index i with pairs (uniform), or nregions.

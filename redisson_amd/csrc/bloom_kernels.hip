@@ -583,10 +583,10 @@ __device__ __forceinline__ uint32_t ht_find(const HTEntry *__restrict__ T, uint3
 // an earlier position of the chunk touches it; the table is consulted only when the prefilter
 // bit is set -- then commit the adds.  Earlier chunks are committed before later ones probe, so
 // chunking keeps the order.  The add list is unordered: owners are resolved by atomicMin.
-constexpr uint32_t kPrefilterBits = 25;  // 4 MiB: mostly L2-resident while the contains run
-
-__device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx) {
-    return (uint32_t)(((((uint64_t)fid << 32) | idx) * 0x9E3779B97F4A7C15ULL) >> (64 - kPrefilterBits));
+// prefilter of 2^pbits bits (rbx_tune "stream_prefilter", default 2^23 = 1 MiB: L2-resident while
+// the contains run, beside the Zipf-hot bitmaps); pshift = 64 - pbits
+__device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx, uint32_t pshift) {
+    return (uint32_t)(((((uint64_t)fid << 32) | idx) * 0x9E3779B97F4A7C15ULL) >> pshift);
 }
 
 // adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t bas
                                                       const FilterDesc *__restrict__ filt,
                                                       const uint32_t *__restrict__ kf, HTEntry *__restrict__ T,
                                                       uint32_t log2cap, uint32_t epoch, uint32_t *__restrict__ zmask,
-                                                      uint32_t *__restrict__ prefilter) {
+                                                      uint32_t *__restrict__ prefilter, uint32_t pshift) {
     const uint32_t na = *nadds;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
@@ -658,8 +658,10 @@ __global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t bas
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
                 zm |= 1u << j;
                 ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], t);
-                const uint32_t pb = prefilter_bit(f.fid, idxs[j]);
-                atomicOr(&prefilter[pb >> 5], 1u << (pb & 31));
+                if (prefilter) {
+                    const uint32_t pb = prefilter_bit(f.fid, idxs[j], pshift);
+                    atomicOr(&prefilter[pb >> 5], 1u << (pb & 31));
+                }
             }
         }
         raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
@@ -674,6 +676,7 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
                                                          const uint8_t *__restrict__ op,
                                                          const HTEntry *__restrict__ T, uint32_t log2cap,
                                                          uint32_t epoch, const uint32_t *__restrict__ prefilter,
+                                                         uint32_t pshift,
                                                          uint8_t *__restrict__ out,
                                                          unsigned long long *__restrict__ counts) {
     uint64_t present = 0;
@@ -704,8 +707,8 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
             for (int u = 0; u < KMAX; ++u) {
                 if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
                     // set by an earlier add of this chunk?  Only possible if the prefilter says so.
-                    const uint32_t pb = prefilter_bit(f.fid, idxs[u]);
-                    if ((prefilter[pb >> 5] >> (pb & 31)) & 1u) {
+                    const uint32_t pb = prefilter_bit(f.fid, idxs[u], pshift);
+                    if (!prefilter || ((prefilter[pb >> 5] >> (pb & 31)) & 1u)) {
                         const uint32_t owner = ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
                         all = owner < (uint32_t)t;
                     } else {
@@ -732,6 +735,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                                                            const uint8_t *__restrict__ op,
                                                            const HTEntry *__restrict__ T, uint32_t log2cap,
                                                            uint32_t epoch, const uint32_t *__restrict__ prefilter,
+                                                           uint32_t pshift,
                                                            uint8_t *__restrict__ out,
                                                            unsigned long long *__restrict__ counts) {
     constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
@@ -839,8 +843,8 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
             if (act[s]) {
                 bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
                 if (clear) {  // set by an earlier add of this chunk?  Only if the prefilter says so.
-                    const uint32_t pb = prefilter_bit(sfid[s], sidx[s]);
-                    if ((prefilter[pb >> 5] >> (pb & 31)) & 1u)
+                    const uint32_t pb = prefilter_bit(sfid[s], sidx[s], pshift);
+                    if (!prefilter || ((prefilter[pb >> 5] >> (pb & 31)) & 1u))
                         clear = !(ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s]) < st[s]);
                 }
                 bool fin = clear;
@@ -1284,7 +1288,7 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
     }
 }
 
-static int g_stream_slots = 0;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel
+static int g_stream_slots = 1;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel (default)
 void set_stream_slots(int v) { g_stream_slots = v; }
 // k_stream_contains runs best at four 256-thread blocks per CU (4 waves/SIMD): the Zipf-hot
 // tenants' bitmaps live in L2, and more resident waves interleave more tenants.  Its registers
@@ -1302,14 +1306,14 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
     hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter);
+                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_qgrid)), dim3(256), 0, st, a.keys,
-                           a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out,
+                           a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out,
                            a.counts);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
-                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.out, a.counts);
+                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts);
     hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
 }

@@ -147,7 +147,8 @@ struct StreamChunkArgs {
     unsigned long long *counts;  // [0] present contains, [1] new adds
     uint32_t *adds;       // nchunk: compacted chunk-local positions of the adds
     uint32_t *nadds;      // 1, zeroed per chunk
-    uint32_t *prefilter;  // 2^25 bits, zeroed per chunk
+    uint32_t *prefilter;  // 2^pbits bits, zeroed per chunk; null: no prefilter (rbx_tune stream_prefilter 0)
+    uint32_t pshift;      // 64 - pbits
 };
 
 // bloom_kernels.hip

@@ -568,7 +568,7 @@ def test_mixed_stream_in_order_semantics(client, fresh, seed, slots):
     try:
         _stream_case(client, fresh, seed)
     finally:
-        L.lib().rbx_tune(b"stream_contains_slots", 0)
+        L.lib().rbx_tune(b"stream_contains_slots", 1)
 
 
 def _stream_case(client, fresh, seed):

@@ -18,6 +18,10 @@ from redisson_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 
+# the engine's defaults (rbx_bench.h rbx_tune), restored after a case that overrides them
+STREAM_SLOTS_DEFAULT = 1
+STREAM_PREFILTER_DEFAULT = 23
+
 
 def _zipf_tenants(rng, nt, n, s=1.0):
     w = 1.0 / np.arange(1, nt + 1, dtype=np.float64) ** s
@@ -26,7 +30,7 @@ def _zipf_tenants(rng, nt, n, s=1.0):
     return np.minimum(np.searchsorted(cdf, rng.random(n)), nt - 1).astype(np.uint32)
 
 
-def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=0, klen=64):
+def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None):
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
@@ -51,12 +55,16 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=0, klen=6
     kf[idx + 1] = kf[idx]
     keys[idx + 1] = keys[idx]
     assert L.lib().rbx_tune(b"stream_chunk", chunk) == 0
-    assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
+    if slots is not None:
+        assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
+    if prefilter is not None:
+        assert L.lib().rbx_tune(b"stream_prefilter", prefilter) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
     finally:
         L.lib().rbx_tune(b"stream_chunk", 0)
-        L.lib().rbx_tune(b"stream_contains_slots", 0)
+        L.lib().rbx_tune(b"stream_contains_slots", STREAM_SLOTS_DEFAULT)
+        L.lib().rbx_tune(b"stream_prefilter", STREAM_PREFILTER_DEFAULT)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -88,12 +96,14 @@ def test_c5_instantiation_two_full_chunks(client, fresh):
     _c5_case(client, fresh, seed=0x5EED0005, nt=200, expected=1_000_000, fpp=1e-3, n=7_000_000)
 
 
+@pytest.mark.parametrize("prefilter", [0, 21, 25])
 @pytest.mark.parametrize("slots", [0, 1])
-def test_c5_kmax8_many_chunks(client, fresh, slots):
+def test_c5_kmax8_many_chunks(client, fresh, slots, prefilter):
     """k = 7 tenants (tryInit(1e6, 0.01): 9,585,058 bits -> k_stream_*<64, 8>), 64-byte keys, 2M commands
-    in 300k-command chunks; both contains kernels (staged, per-lane slots)."""
-    _c5_case(client, fresh, seed=77 + slots, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000, chunk=300_000,
-             slots=slots)
+    in 300k-command chunks; both contains kernels (staged, per-lane slots), with and without the
+    prefilter in front of the first-setter table."""
+    _c5_case(client, fresh, seed=77 + slots + 2 * prefilter, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000,
+             chunk=300_000, slots=slots, prefilter=prefilter)
 
 
 def test_c5_k10_chunk_boundaries(client, fresh):
