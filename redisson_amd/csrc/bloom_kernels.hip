@@ -1290,6 +1290,10 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
 
 static int g_stream_slots = 1;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel (default)
 void set_stream_slots(int v) { g_stream_slots = v; }
+// The slot stream kernel at P = 2, Q = 2 (120 VGPRs, four blocks per CU) on 1024 blocks, one
+// resident round: C5 9.91 (2048) -> 9.67 ms; shapes 32 / 42 / 24: 10.8 / 11.2 / 11.2 ms
+// (profiles/r03/r03u_c5sweep_qshape_qgrid.jsonl).
+static unsigned g_stream_qgrid = 1024;
 // k_stream_contains runs best at four 256-thread blocks per CU (4 waves/SIMD): the Zipf-hot
 // tenants' bitmaps live in L2, and more resident waves interleave more tenants.  Its registers
 // (93 VGPRs since the r02 hash) would admit five, so the launch reserves 33,000 bytes of dynamic
@@ -1308,9 +1312,9 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
     if (g_stream_slots)
-        hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_qgrid)), dim3(256), 0, st, a.keys,
-                           a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out,
-                           a.counts);
+        hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
+                           a.keys, a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
+                           a.pshift, a.out, a.counts);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts);
