@@ -730,7 +730,7 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
 // no lane time, and a clear bit consults the prefilter / first-setter table exactly as above.
 template <int KLEN, int P, int Q>
 __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_t base, uint64_t nchunk,
-                                                           const FilterDesc *__restrict__ filt,
+                                                           const ProbeDesc *__restrict__ pdesc,
                                                            const uint32_t *__restrict__ kf,
                                                            const uint8_t *__restrict__ op,
                                                            const HTEntry *__restrict__ T, uint32_t log2cap,
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                     hash_key<KLEN>(keys, base + t, e.h1, e.h2);
                     e.t = (uint32_t)t;
                     e.fi = kf[base + t];
-                    e.idx0 = mod63(e.h1 & 0x7fffffffffffffffULL, filt[e.fi].mp);
+                    e.idx0 = mod63c(e.h1 & 0x7fffffffffffffffULL, pdesc[e.fi].mc);
                     qb[b * RANGE + qlen[b] + (uint32_t)__popcll(mask & lt)] = e;
                 }
                 qlen[b] += (uint32_t)__popcll(mask);
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
                 if (need && rank < avail) {
                     const QEnt e = qb[cur * RANGE + qpos + rank];
-                    const FilterDesc f = filt[e.fi];
+                    const ProbeDesc f = pdesc[e.fi];
                     act[s] = true;
                     need = false;
                     sh1[s] = e.h1;
@@ -818,7 +818,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                     st[s] = e.t;
                     sidx[s] = e.idx0;
                     sbm[s] = f.bm;
-                    smp[s] = mod_compact(f.mp);
+                    smp[s] = f.mc;
                     sjk[s] = f.k << 16;
                     sfid[s] = f.fid;
                 }
@@ -1313,7 +1313,7 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                        a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
-                           a.keys, a.base, a.nchunk, a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
+                           a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
                            a.pshift, a.out, a.counts);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,

@@ -177,6 +177,7 @@ struct rbx_ctx {
 
     // staging for host-buffer calls
     DevBuf keys_bytes, keys_offs, out_bytes, seg_offs, counters, filt_table, ptrs, histo, misc, tile_segs, hll_tiles;
+    DevBuf probe_table;  // ProbeDesc per entry of filt_table
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf pa_stamps;  // add_partition_diag & 64: region-pass phase times (rbx_bench_add_stamps)
@@ -806,7 +807,7 @@ int rbx_shutdown(rbx_ctx *c) {
         c->hll_free.clear();
         c->slab.reset();  // bitmaps still held by open handles keep their slab alive
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
-                          &c->counters, &c->filt_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
+                          &c->counters, &c->filt_table, &c->probe_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
@@ -1389,6 +1390,10 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
         RBX_TRY(c->filt_table.reserve(v.size() * sizeof(FilterDesc)));
         // pageable source: the runtime has staged it when the call returns
         HIP_TRY(hipMemcpyAsync(c->filt_table.p, v.data(), v.size() * sizeof(FilterDesc), hipMemcpyHostToDevice, st));
+        std::vector<ProbeDesc> pd(v.size());
+        for (size_t s = 0; s < v.size(); ++s) pd[s] = ProbeDesc{v[s].bm, mod_compact(v[s].mp), v[s].k, v[s].fid};
+        RBX_TRY(c->probe_table.reserve(pd.size() * sizeof(ProbeDesc)));
+        HIP_TRY(hipMemcpyAsync(c->probe_table.p, pd.data(), pd.size() * sizeof(ProbeDesc), hipMemcpyHostToDevice, st));
         c->filt_cache.swap(v);
         c->filt_generation = c->ks.generation;
     }
@@ -1494,6 +1499,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
         s.base = base;
         s.nchunk = nch;
         s.filt = c->filt_table.as<FilterDesc>();
+        s.pdesc = c->probe_table.as<ProbeDesc>();
         s.kf = d_key_filter;
         s.op = d_key_op;
         s.table = c->table.as<HTEntry>();

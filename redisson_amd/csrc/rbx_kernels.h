@@ -27,6 +27,17 @@ struct FilterDesc {
     uint32_t fid;  // identity in the first-setter table (unique per filter within a call)
 };
 
+// The per-filter fields a probing kernel reads, in one 32-byte line-aligned record (FilterDesc is 56
+// bytes with the 64-bit modulus and the Redis-length pointer): the ordered stream's contains reads
+// one per command of a random (Zipf) tenant.
+struct alignas(32) ProbeDesc {
+    const uint32_t *bm;
+    ModC mc;
+    uint32_t k;
+    uint32_t fid;
+};
+static_assert(sizeof(ProbeDesc) == 32, "one half line");
+
 struct alignas(16) HTEntry {
     unsigned long long tag;  // [63:56] epoch, [55:32] fid, [31:0] bit index
     unsigned long long idw;  // [63:32] 254 - epoch, [31:0] min key id
@@ -137,6 +148,7 @@ struct StreamChunkArgs {
     KeysDev keys;
     uint64_t base, nchunk;
     const FilterDesc *filt;
+    const ProbeDesc *pdesc;  // the same filters' probe fields (stream contains)
     const uint32_t *kf;   // per key: index into filt
     const uint8_t *op;    // per key: 0 contains, 1 add
     HTEntry *table;
