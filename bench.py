@@ -700,6 +700,8 @@ def run_c3(args, world, rank, local, steps, warmup):
     del tbl
     algo = n * (16 + k * 8)
     achieved = algo / (ms / 1e3) / 1e9
+    # PMC counts of profiles/traffic.json are of the default workload's calls only
+    tj = args.traffic_json if (args.keys, args.tenants, world) == (100_000_000, 100_000, 1) else None
     # 180 GB of bitmaps: the slot kernel unless a staged schedule was forced
     slots = args.stage1 is None or args.stage1 == 5
     kname = "k_bloom_contains_q" if slots else "k_bloom_contains_multi"
@@ -716,11 +718,10 @@ def run_c3(args, world, rank, local, steps, warmup):
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_traffic(args.traffic_json, kname, "hbm_bytes_by_class") or
-                     load_traffic(args.traffic_json, kname),
+                     "traffic": load_traffic(tj, kname, "hbm_bytes_by_class") or load_traffic(tj, kname),
                      "kernel": kdesc, "kernel_avg_ms": ms,
                      "request_peak_kind": "k_gather_segments: 4 random loads per key inside its tenant's slice",
-                     **request_fields(args.traffic_json, kname, ms, peak, stream_write_peak(client, 1 << 30, stream))},
+                     **request_fields(tj, kname, ms, peak, stream_write_peak(client, 1 << 30, stream))},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
     for h in handles:
@@ -799,6 +800,9 @@ def run_c5(args, world, rank, local, steps, warmup):
                gather_peak(client, 512 << 20, n, 7, stream, g))
     del tbl
     algo = n * (64 + 10 * 8)
+    # PMC counts of profiles/traffic.json are of the default workload's calls only
+    tj = args.traffic_json if (n, args.tenants, world, args.zipf_s, args.add_fraction) == \
+        (100_000_000, 100_000, 1, 1.0, 0.1) else None
     res = {
         "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
         "value": value, "unit": "ops/s", "n_gpus": world, "steps": steps, "warmup": warmup,
@@ -811,12 +815,12 @@ def run_c5(args, world, rank, local, steps, warmup):
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": load_traffic(args.traffic_json, "stream_pipeline", "hbm_bytes_by_class") or
-                     load_traffic(args.traffic_json, "stream_pipeline"),
-                     "kernel": "k_stream_probe + k_stream_contains + k_stream_commit", "kernel_avg_ms": ms,
+                     "traffic": load_traffic(tj, "stream_pipeline", "hbm_bytes_by_class") or
+                     load_traffic(tj, "stream_pipeline"),
+                     "kernel": "k_stream_compact + k_stream_probe + k_stream_contains_q + k_stream_commit", "kernel_avg_ms": ms,
                      "request_peak_kind": "max(k_gather_segments one key per tenant slice, k_gather_probe "
                                           "over 512 MiB) for reads; k_stream_write for writes",
-                     **request_fields(args.traffic_json, "stream_pipeline", ms, peak,
+                     **request_fields(tj, "stream_pipeline", ms, peak,
                                       stream_write_peak(client, 1 << 30, stream))},
     }
     for h in handles:
@@ -935,8 +939,9 @@ def run_c4(args, world, rank, local, steps, warmup):
                    "elements_per_gpu": n, "parallelism": f"element-partitioned x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_traffic(args.traffic_json, "k_hll_pfadd", "hbm_bytes_by_class") or
-                     load_traffic(args.traffic_json, "k_hll_pfadd"),
+                     "traffic": (load_traffic(args.traffic_json, "k_hll_pfadd", "hbm_bytes_by_class") or
+                                 load_traffic(args.traffic_json, "k_hll_pfadd"))
+                     if (args.elements, world) == (1_000_000_000, 1) else None,
                      "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms,
                      # elems/s x 16 B / the measured HBM stream-read peak
                      "stream_read_peak_GBps": peak_gbs, "stream_frac": achieved / peak_gbs},
