@@ -58,7 +58,9 @@ template <int KMAX> constexpr int ba_per() { return KMAX <= 8 ? 2 : 1; }
 constexpr int kBaS1Threads = 512;  // 1024 keys per tile (KMAX 8): 64 KiB image, two blocks per CU
 // (2048-key tiles, one block per CU: 1.76 -> 1.89 ms)
 
-template <int KLEN, int KMAX>
+// PF (fixed-length keys): the next tile's key bytes are loaded into registers right after this
+// tile's hash, so they arrive during its count / reserve / place / store phases.
+template <int KLEN, int KMAX, bool PF>
 __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64_t base, uint64_t nchunk, FilterDesc f,
                                                    uint32_t s1, uint32_t ncoarse, uint64_t cap1,
                                                    unsigned long long *__restrict__ p1, uint32_t *__restrict__ cnt1,
@@ -71,6 +73,23 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
     const uint32_t sub = blockIdx.x % kBaSub;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t maxidx = 0;
+    constexpr bool KP = PF && KLEN > 0;
+    constexpr int NV = KLEN > 0 ? KLEN / 16 : 1;
+    uint4 kx[PER][NV];
+    auto load_keys = [&](uint64_t tl) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint64_t t = tl * TILE + threadIdx.x + q * NT;
+            if (t < nchunk) {
+                const uint4 *v = (const uint4 *)(keys.bytes + (base + t) * (uint64_t)(KLEN > 0 ? KLEN : 16));
+#pragma unroll
+                for (int j = 0; j < NV; ++j) kx[q][j] = ld_nt16(v + j);
+            }
+        }
+    };
+    if constexpr (KP) {
+        if ((uint64_t)blockIdx.x < ntiles) load_keys(blockIdx.x);
+    }
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         if (threadIdx.x < 256) s_cnt[threadIdx.x] = 0;
         const uint64_t t0 = tile * TILE + threadIdx.x;
@@ -79,13 +98,20 @@ __global__ __launch_bounds__(kBaS1Threads) void k_ba_stage1(KeysDev keys, uint64
         for (int q = 0; q < PER; ++q) {
             const uint64_t t = t0 + q * NT;
             uint64_t h1 = 0, h2 = 0;
-            if (t < nchunk) bk_hash<KLEN>(keys, base + t, h1, h2);
+            if constexpr (KP) {
+                if (t < nchunk) hh128_regs<(KLEN > 0 ? KLEN : 16)>(kx[q], h1, h2);
+            } else {
+                if (t < nchunk) bk_hash<KLEN>(keys, base + t, h1, h2);
+            }
             uint64_t h = h1;
 #pragma unroll
             for (int j = 0; j < KMAX; ++j) {
                 if ((uint32_t)j < f.k) idx[q][j] = mod63(h & 0x7fffffffffffffffULL, f.mp);
                 h += (j & 1) ? h1 : h2;
             }
+        }
+        if constexpr (KP) {
+            if (tile + gridDim.x < ntiles) load_keys(tile + gridDim.x);
         }
         __syncthreads();  // s_cnt reset visible
 #pragma unroll
@@ -177,7 +203,7 @@ __device__ __forceinline__ void ba_put_region(unsigned long long e, uint64_t reg
 // 16K-pair tiles, one 1024-thread block per CU (8K-pair tiles at two blocks per CU, each
 // overlapping the other's loads, measured 1.65 -> 1.78 ms).  A slot's bucket is read back from its
 // pair (no bucket byte array).
-template <bool P6, bool STAMP>
+template <bool P6, bool STAMP, bool PF>
 __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned long long *__restrict__ pin,
                                                      const uint32_t *__restrict__ cnt_in, uint64_t cap_in,
                                                      uint32_t nparents, uint32_t sub_div, uint32_t items_per_part,
@@ -194,26 +220,45 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
     const uint32_t nf = 1u << fo, fmask = nf - 1;
     const uint32_t nparts = nparents * sub_div;
     const uint32_t nitems = nparts * items_per_part;
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const uint32_t it = item / nparts, ix = item - it * nparts;
-        const uint32_t parent = ix % nparents, part = parent * sub_div + ix / nparents;
-        const uint64_t nc = min<uint64_t>(cnt_in[part], cap_in);
-        const uint64_t start = (uint64_t)it * TILE;
-        if (start >= nc) continue;  // uniform over the block
-        const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
-        if (threadIdx.x < 256) s_cnt[threadIdx.x] = 0;
-        __syncthreads();
+    struct Item {
+        uint32_t parent, part, m;
+        uint64_t start;
+    };
+    auto find_item = [&](uint32_t from, Item &ii) -> uint32_t {  // uniform: the next item with pairs
+        for (uint32_t item = from; item < nitems; item += gridDim.x) {
+            const uint32_t it = item / nparts, ix = item - it * nparts;
+            ii.parent = ix % nparents;
+            ii.part = ii.parent * sub_div + ix / nparents;
+            const uint64_t nc = min<uint64_t>(cnt_in[ii.part], cap_in);
+            ii.start = (uint64_t)it * TILE;
+            if (ii.start < nc) {
+                ii.m = (uint32_t)min<uint64_t>(TILE, nc - ii.start);
+                return item;
+            }
+        }
+        return nitems;
+    };
+    unsigned long long e[2 * PER];
+    auto load_tile = [&](const Item &ii) {
         // cap_in is a multiple of TILE: the tile is 16-byte aligned
-        const u32x4 *src = (const u32x4 *)(pin + (uint64_t)part * cap_in + start);
-        unsigned long long e[2 * PER];
+        const u32x4 *src = (const u32x4 *)(pin + (uint64_t)ii.part * cap_in + ii.start);
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
             const uint32_t q = 2 * (p * NT + threadIdx.x);
             u32x4 v = {0u, 0u, 0u, 0u};
-            if (q < m) v = __builtin_nontemporal_load(src + p * NT + threadIdx.x);
+            if (q < ii.m) v = __builtin_nontemporal_load(src + p * NT + threadIdx.x);
             e[2 * p] = w2(v.x, v.y);
             e[2 * p + 1] = w2(v.z, v.w);
         }
+    };
+    Item cur{};
+    uint32_t item = find_item(blockIdx.x, cur);
+    if (PF && item < nitems) load_tile(cur);
+    while (item < nitems) {
+        const uint32_t parent = cur.parent, m = cur.m;
+        if (threadIdx.x < 256) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        if (!PF) load_tile(cur);
 #pragma unroll
         for (int p = 0; p < 2 * PER; ++p) {
             const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
@@ -239,6 +284,11 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
                 s_img[slot] = e[p];
             }
         }
+        // PF: the next item's tile is loaded into the pair registers (free after the placement),
+        // so the load flies during this tile's stores instead of stalling the next tile's count
+        Item nxt{};
+        const uint32_t nitem = find_item(item + gridDim.x, nxt);
+        if (PF && nitem < nitems) load_tile(nxt);
         // the reservation results reach LDS only now: the placement above overlapped their round trip
         if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) s_gb[threadIdx.x - 256] = gb;
         __syncthreads();
@@ -252,6 +302,8 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
         }
         __syncthreads();
         ps.mark(3);
+        item = nitem;
+        cur = nxt;
     }
     ps.flush(stamps);
 }
@@ -919,6 +971,14 @@ void set_add_region_kernel(int v) { g_region_kernel = v; }
 // reports a region's owners by direct atomics instead (default and maximum kBa6Main)
 static uint32_t g_rec_limit = kBa6Main;
 void set_add_rec_lds_limit(int v) { g_rec_limit = (uint32_t)v; }
+// EXPERIMENTS (rbx_tune "add_rebucket_prefetch"): 1 = the next tile's loads issued after the
+// placement (default), 0 = at the top of each tile
+static int g_rebucket_prefetch = 1;
+void set_add_rebucket_prefetch(int v) { g_rebucket_prefetch = v; }
+// EXPERIMENTS (rbx_tune "add_stage1_prefetch"): 1 = stage 1 loads the next tile's fixed-length keys
+// into registers after this tile's hash (default), 0 = each tile loads its own
+static int g_stage1_prefetch = 1;
+void set_add_stage1_prefetch(int v) { g_stage1_prefetch = v; }
 
 template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
@@ -926,17 +986,24 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     const uint64_t ntiles = (a.nchunk + TILE - 1) / TILE;
     hipLaunchKernelGGL(k_ba_mode, dim3(1), dim3(1024), 0, st, (const uint32_t *)a.f.bm, a.nwords4, a.record_policy,
                        a.mode);
-    hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)), dim3(kBaS1Threads), 0, st,
-                       a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1, a.overflow);
+    if (g_stage1_prefetch)
+        hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, true>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
+                           dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
+                           a.overflow);
+    else
+        hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, false>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
+                           dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
+                           a.overflow);
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
     const dim3 rgrid(std::min<uint32_t>(a.nregions, g_region_grid));
     unsigned long long *rst = a.stamps ? a.stamps + 8 : nullptr;
-#define BA_REBUCKET(P6, ST)                                                                                         \
-    hipLaunchKernelGGL((k_ba_rebucket<P6, ST>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, \
+#define BA_REBUCKET(P6, ST, PF)                                                                                          \
+    hipLaunchKernelGGL((k_ba_rebucket<P6, ST, PF>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, \
                        kBaSub, it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
-    if (g_region_kernel == 1) BA_REBUCKET(false, false);
-    else if (a.stamps) BA_REBUCKET(true, true);
-    else BA_REBUCKET(true, false);
+    if (g_region_kernel == 1) BA_REBUCKET(false, false, false);
+    else if (a.stamps) BA_REBUCKET(true, true, true);
+    else if (g_rebucket_prefetch) BA_REBUCKET(true, false, true);
+    else BA_REBUCKET(true, false, false);
 #undef BA_REBUCKET
     if (g_region_kernel == 1) {
         if (a.stamps)

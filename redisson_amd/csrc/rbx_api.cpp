@@ -2949,6 +2949,16 @@ int rbx_tune(const char *key, int value) {
         set_add_region_kernel(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "add_stage1_prefetch")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_stage1_prefetch in {0, 1}");
+        set_add_stage1_prefetch(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_rebucket_prefetch")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rebucket_prefetch in {0, 1}");
+        set_add_rebucket_prefetch(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "add_rec_lds_limit")) {
         if (value < 0 || value > 7168) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rec_lds_limit in [0, 7168]");
         set_add_rec_lds_limit(value);

@@ -318,17 +318,13 @@ __device__ __forceinline__ void hh128_bytes(const uint8_t *p, uint64_t len, uint
     hh_finalize128(s, h1, h2);
 }
 
-// HighwayHash128 of a fixed-length key at a 16-byte aligned address (fast path).
+// HighwayHash128 of a fixed-length key already in registers (L/16 little-endian 16-byte words).
 template <int L>
-__device__ __forceinline__ void hh128_fixed(const uint8_t *p, uint64_t &h1, uint64_t &h2) {
+__device__ __forceinline__ void hh128_regs(const uint4 (&x)[L / 16], uint64_t &h1, uint64_t &h2) {
     static_assert(L % 16 == 0 && L > 0, "fast path needs 16-byte multiples");
     HH s;
     hh_reset(s);
-    const uint4 *v = (const uint4 *)p;
     constexpr int NV = L / 16;
-    uint4 x[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) x[j] = ld_nt16(v + j);
 #pragma unroll
     for (int pk = 0; pk + 1 < NV; pk += 2) {
         const uint32_t w[8] = {x[pk].x, x[pk].y, x[pk].z, x[pk].w,
@@ -342,6 +338,17 @@ __device__ __forceinline__ void hh128_fixed(const uint8_t *p, uint64_t &h1, uint
         hh_packet(s, w);
     }
     hh_finalize128(s, h1, h2);
+}
+
+// HighwayHash128 of a fixed-length key at a 16-byte aligned address (fast path).
+template <int L>
+__device__ __forceinline__ void hh128_fixed(const uint8_t *p, uint64_t &h1, uint64_t &h2) {
+    static_assert(L % 16 == 0 && L > 0, "fast path needs 16-byte multiples");
+    const uint4 *v = (const uint4 *)p;
+    uint4 x[L / 16];
+#pragma unroll
+    for (int j = 0; j < L / 16; ++j) x[j] = ld_nt16(v + j);
+    hh128_regs<L>(x, h1, h2);
 }
 
 // ---------------------------------------------------------------------------------

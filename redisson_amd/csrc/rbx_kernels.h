@@ -109,6 +109,8 @@ void set_contains_stage1_per(int v);  // 1 or 2 (default)
 void set_add_region_grid(int v);  // 256..65536 (default 2048)
 void set_add_region_kernel(int v);  // 1 (r02 8-byte pairs) or 2 (default: 6-byte pairs, pipelined)
 void set_add_rec_lds_limit(int v);  // 0..7168 (tests)
+void set_add_rebucket_prefetch(int v);  // 0 or 1
+void set_add_stage1_prefetch(int v);  // 0 or 1
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 // Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB

@@ -288,7 +288,8 @@ def main():
                 for kv in filter(None, ("" if v == "-" else v).split(",")):
                     key = kv.split("=")[0]
                     L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2, "add_region_kernel": 2,
-                                                       "add_region_grid": 2048, "add_rec_lds_limit": 7168}.get(key, 0))
+                                                       "add_region_grid": 2048, "add_rec_lds_limit": 7168,
+                                                       "add_rebucket_prefetch": 1, "add_stage1_prefetch": 1}.get(key, 0))
         assert len(set(news.values())) == 1, news
         for v, t in res.items():
             med = statistics.median(t)
