@@ -234,14 +234,16 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
 // fine bucket = region within c.  Items are numbered c-minor so the blocks running at one time
 // reserve from different buckets' region counters.  Runs are whole lines (kBkLine2 pairs), the
 // remainder carries to the next tile (s_car), the item's last remainders are padded.
-template <int NT, int PER>
+template <int NT, int PER, bool STAMP>
 __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__restrict__ pairs1,
                                                   const uint32_t *__restrict__ cnt1, uint64_t cap1, uint32_t ncoarse,
                                                   uint32_t fb, uint32_t nregions, uint64_t cap2,
                                                   uint32_t *__restrict__ p2lo, uint16_t *__restrict__ p2hi,
                                                   uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
-                                                  uint32_t flags) {
+                                                  uint32_t flags, unsigned long long *__restrict__ stamps) {
+    PhaseStamps<STAMP, 4> ps;
+    ps.start();
     // PER u32x4 (two pairs each) per thread
     constexpr uint32_t TILE = 2 * PER * NT;
     __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
@@ -291,6 +293,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                 if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + kBkRegionBits)) & fmask], 1u);
             }
             __syncthreads();
+            ps.mark(0);
             // the reservation atomics are issued here and their results stored to LDS only after
             // the placement below, which overlaps their round trip (one 1024-thread block per CU:
             // a blocking reservation idled the CU); the next tile's loads follow the atomics
@@ -305,6 +308,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
             }
             if (start + TILE < nc) load(start + TILE);
             __syncthreads();
+            ps.mark(1);
 #pragma unroll
             for (int p = 0; p < 2 * PER; ++p) {
                 const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
@@ -315,6 +319,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
             }
             if (threadIdx.x >= 128 && threadIdx.x - 128 < nf) s_gb[threadIdx.x - 128] = gb;
             __syncthreads();
+            ps.mark(2);
             for (uint32_t f = wave; f < nf; f += NT / 64) {
                 const uint32_t n = s_cnt[f], cn = s_cn[f], full = s_full[f], st = s_start[f];
                 const uint64_t rb = (uint64_t)((c << fb) + f) * cap2;
@@ -332,6 +337,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
             }
             par ^= 1u;
             __syncthreads();
+            ps.mark(3);
         }
         for (uint32_t f = wave; f < nf; f += NT / 64) {  // the item's last remainders, padded
             const uint32_t cn = s_cn[f];
@@ -345,7 +351,9 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                         p2hi + (uint64_t)r * cap2, cap2, bm, miss);
         }
         __syncthreads();  // s_cn / s_car reuse by the next item
+        ps.mark(3);
     }
+    ps.flush(stamps);
 }
 
 // K4 -----------------------------------------------------------------------------------
@@ -379,13 +387,16 @@ __device__ __forceinline__ void bk_test6(const uint32_t *s_bm, uint32_t lo, uint
 
 // One block per region; a lane reads 4 pairs at a time (16 B of lo words + 8 B of hi halves),
 // 6 groups per round trip, the first round issued together with the region's bitmap load.
+template <bool STAMP>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_bk_probe(const uint32_t *__restrict__ p2lo,
                                                    const uint16_t *__restrict__ p2hi,
                                                    const uint32_t *__restrict__ cnt2, uint64_t cap2, uint32_t nregions,
                                                    const uint32_t *__restrict__ bm, uint64_t nwords4,
                                                    unsigned long long *__restrict__ miss, uint32_t *__restrict__ mrec,
                                                    uint32_t *__restrict__ mcnt, uint64_t capm, uint32_t nmranges,
-                                                   uint32_t flags) {
+                                                   uint32_t flags, unsigned long long *__restrict__ stamps) {
+    PhaseStamps<STAMP, 4> ps;
+    ps.start();
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
     // <= 80 KiB so two blocks share a CU: the bucketed image of the miss records reuses the
     // region bitmap's LDS once the region's probes are done
@@ -427,6 +438,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             }
         }
         __syncthreads();  // waits for the bitmap DMA (and the first pair loads)
+        ps.mark(0);
         for (uint32_t base = 0;;) {
 #pragma unroll
             for (uint32_t u = 0; u < G; ++u) {
@@ -451,6 +463,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             }
         }
         __syncthreads();
+        ps.mark(1);
         const uint32_t nm = min(s_mn, kBkMissBuf);
         if (nm) {  // uniform: bucket the region's miss records by key range
             if (threadIdx.x < 256) s_mc[threadIdx.x] = 0;
@@ -479,7 +492,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             }
         }
         __syncthreads();  // s_bm / s_mrec / s_mn reuse
+        ps.mark(2);
     }
+    ps.flush(stamps);
 }
 
 // K5 -----------------------------------------------------------------------------------
@@ -567,8 +582,14 @@ static void bk_stage1(const PcArgs &a, hipStream_t st) {
 template <int NT2, int PER>
 static void bk_emit2(const PcArgs &a, hipStream_t st) {
     // one block per (coarse bucket, sub-partition); tiles start 16-byte aligned (cap1 is a multiple of 8192)
-    hipLaunchKernelGGL((k_bk_emit2<NT2, PER>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1, a.cap1,
-                       a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags);
+    if (a.stamps)
+        hipLaunchKernelGGL((k_bk_emit2<NT2, PER, true>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1,
+                           a.cap1, a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags,
+                           a.stamps);
+    else
+        hipLaunchKernelGGL((k_bk_emit2<NT2, PER, false>), dim3(a.ncoarse * kBkSub), dim3(NT2), 0, st, a.pairs1, a.cnt1,
+                           a.cap1, a.ncoarse, a.fb, a.nregions, a.cap2, a.p2lo, a.p2hi, a.cnt2, a.bm, a.miss, a.flags,
+                           nullptr);
 }
 
 // EXPERIMENTS (rbx_tune "contains_emit2_nt"): emit2 shape.  1536 (default): 1024 threads, 12K-pair
@@ -590,8 +611,14 @@ static void bk_chunk(const PcArgs &a, hipStream_t st) {
     else if (g_emit2_nt == 1024) bk_emit2<1024, 4>(a, st);  // 8K-pair tiles
     else if (g_emit2_nt == 1792) bk_emit2<1024, 7>(a, st);  // 14K-pair tiles
     else bk_emit2<1024, 6>(a, st);                          // 12K-pair tiles (default)
-    hipLaunchKernelGGL(k_bk_probe, dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo, a.p2hi, a.cnt2,
-                       a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges, a.flags);
+    if (a.stamps)
+        hipLaunchKernelGGL((k_bk_probe<true>), dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo,
+                           a.p2hi, a.cnt2, a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges,
+                           a.flags, a.stamps + 8);
+    else
+        hipLaunchKernelGGL((k_bk_probe<false>), dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo,
+                           a.p2hi, a.cnt2, a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges,
+                           a.flags, nullptr);
     hipLaunchKernelGGL(k_bk_misses, dim3(2048), dim3(1024), 0, st, a.mrec, a.mcnt, a.capm, a.nmranges, a.miss);
     hipLaunchKernelGGL(k_bk_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.alive, a.miss, a.nchunk, a.base,
                        a.out, a.count);

@@ -704,6 +704,13 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
         a.out = d_out;
         a.count = d_count;
         a.flags = (uint32_t)g_partition_flags;
+        if (a.flags & 64) {
+            if (c->pa_stamps.cap == 0) {
+                RBX_TRY(c->pa_stamps.reserve(16 * 8));
+                HIP_TRY(hipMemsetAsync(c->pa_stamps.p, 0, 16 * 8, st));
+            }
+            a.stamps = c->pa_stamps.as<unsigned long long>();
+        }
         HIP_TRY(hipMemsetAsync(a.miss, 0, ngroups * 8, st));
         HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
         launch_contains_partitioned_chunk(a, fl, st);
@@ -2870,8 +2877,8 @@ int rbx_tune(const char *key, int value) {
     // DIAGNOSTICS ONLY (tools/microbench.py pflags), results become wrong: 4 = stage 1 emits no
     // pairs, 8 = the probe records no misses.  0 = normal operation.
     if (!strcmp(key, "contains_partition_flags")) {
-        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16 && value != 32)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16, 32}");
+        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16 && value != 32 && value != 64)
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16, 32, 64}");
         g_partition_flags = value;
         return RBX_OK;
     }

@@ -98,6 +98,7 @@ struct PcArgs {
     uint8_t *out;
     unsigned long long *count;
     uint32_t flags;  // diagnostics only (rbx_tune "contains_partition_flags"); 0 in normal operation
+    unsigned long long *stamps;  // flags & 64: emit2 / probe phase times (rbx_bench_add_stamps), else null
 };
 inline unsigned grid_for_pc(uint64_t n) {
     uint64_t g = ((n + 63) / 64 + 255) / 256;

@@ -263,6 +263,38 @@ def main():
         L.lib().rbx_tune(b"add_partition_diag", 0)
         L.lib().rbx_tune(b"add_region_kernel", 2)
 
+    if "pcstamp" in a.what:
+        # partitioned contains phase times (contains_partition_flags 64, exact results), C2 contains
+        # of n keys against a 2^32-bit filter holding n/2: emit2 (count, scan/reserve, place, store)
+        # and probe (top wait, probe loop, miss records) shares of block time
+        import ctypes as C
+
+        cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+        fb = client.getBloomFilter("pcs")
+        fb.tryInitRaw(1 << 32, 7)
+        h = BloomHandle(client, "pcs")
+        h.add_dev(device_keys(keys.data_ptr(), n // 2, 32), cnt.data_ptr(), stream=sp)
+        dk = device_keys(keys.data_ptr(), n, 32)
+        buf = (C.c_ulonglong * 16)()
+        for fl in (0, 64, 0, 64):
+            assert L.lib().rbx_tune(b"contains_partition_flags", fl) == 0
+            L.lib().rbx_bench_add_stamps(client.ctx, buf, 16)  # clear
+            cnt[2:].zero_()
+            ms = timed(stream, lambda: h.contains_dev(dk, cnt.data_ptr() + 16, stream=sp), 1)
+            assert L.lib().rbx_bench_add_stamps(client.ctx, buf, 16) == 0
+            etot = sum(buf[:4])
+            ptot = sum(buf[8:11])
+            print(json.dumps({"bench": "pcstamp", "flags": fl, "ms": ms, "present": int(cnt[2].item()),
+                              "emit2_share": {nm: buf[i] / max(etot, 1) for i, nm in
+                                              enumerate(["count", "scan_reserve", "place", "store"])},
+                              "emit2_ticks_per_cu": etot / 256,
+                              "probe_share": {nm: buf[8 + i] / max(ptot, 1) for i, nm in
+                                              enumerate(["top_wait", "probe", "miss_records"])},
+                              "probe_ticks_per_cu": ptot / 256}), flush=True)
+        L.lib().rbx_tune(b"contains_partition_flags", 0)
+        h.close()
+        fb.delete()
+
     if "addab" in a.what:
         # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
         # round, fresh filter per run: RBX_ADDAB="key=v,key=v;key=v" ("-" = defaults)
