@@ -57,6 +57,12 @@ def _load():
         "orc_hll_histogram": (None, [u8p, C.POINTER(C.c_int)]),
         "orc_hll_count": (C.c_uint64, [u8p]),
         "orc_hll_merge": (None, [u8p, u8p]),
+        "orc_hll_sparse_set": (C.c_int, [u8p, C.POINTER(C.c_size_t), C.c_size_t, C.c_long, C.c_int, C.c_size_t]),
+        "orc_hll_sparse_new": (C.c_size_t, [u8p]),
+        "orc_hll_sparse_pfadd": (C.c_int, [u8p, C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(C.c_int), u8p, u8p,
+                                           u64p, C.c_uint64, C.c_size_t]),
+        "orc_hll_sparse_merge": (C.c_int, [u8p, C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(C.c_int), u8p,
+                                           C.c_size_t]),
         "orc_murmur_batch": (None, [u8p, u64p, C.c_uint64, u64p]),
         "orc_bloom_contains_mt": (C.c_int64, [u8p, C.c_uint64, u8p, u64p, C.c_uint64, C.c_int, C.c_int64, u8p,
                                               C.c_int]),
@@ -369,3 +375,59 @@ def hll_dense_unpack(data: bytes) -> np.ndarray:
     out = hll_new()
     lib().orc_hll_dense_unpack(_p(src), _p(out))
     return out
+
+
+HLL_SPARSE_MAX_BYTES = 3000  # redis.conf hll-sparse-max-bytes (default)
+
+
+class RedisHll:
+    """One Redis HLL key as redis-server holds it [redis-7.2 hyperloglog.c, external; restated in
+    rbx_oracle.c orc_hll_sparse_*]: created sparse (createHLLObject), every PFADD element applied
+    in order through hllSparseSet until the first promotion, dense afterwards.  `regs` tracks the
+    registers in both encodings; `string(card)` is the GET value."""
+
+    CAP = 16384 + 8  # an opcode covers >= 1 register
+
+    def __init__(self, max_bytes: int = HLL_SPARSE_MAX_BYTES):
+        self.ops = np.zeros(self.CAP, np.uint8)
+        self.len = C.c_size_t(lib().orc_hll_sparse_new(_p(self.ops)))
+        self.dense = C.c_int(0)
+        self.regs = hll_new()
+        self.max_bytes = max_bytes
+
+    @classmethod
+    def from_string(cls, s: bytes, max_bytes: int = HLL_SPARSE_MAX_BYTES):
+        h = cls(max_bytes)
+        if s[4] == 0:
+            h.dense.value = 1
+            h.regs = hll_dense_unpack(s[16:])
+        else:
+            h.regs = hll_sparse_unpack(s[16:])
+            h.ops[:len(s) - 16] = np.frombuffer(s[16:], np.uint8)
+            h.len.value = len(s) - 16
+        return h
+
+    def pfadd(self, buf, offs) -> int:
+        r = lib().orc_hll_sparse_pfadd(_p(self.ops), C.byref(self.len), self.CAP, C.byref(self.dense), _p(self.regs),
+                                       _p(buf), _p(offs, u64p), offs.size - 1, self.max_bytes)
+        assert r >= 0, "invalid sparse string"
+        return r
+
+    def merge_from(self, maxregs: np.ndarray, use_dense: bool) -> None:
+        """pfmergeCommand's write-back: maxregs = max over the sources and this key."""
+        if use_dense:
+            self.dense.value = 1
+        if not self.dense.value:
+            assert lib().orc_hll_sparse_merge(_p(self.ops), C.byref(self.len), self.CAP, C.byref(self.dense),
+                                              _p(np.ascontiguousarray(maxregs, dtype=np.uint8)), self.max_bytes) == 0
+        self.regs = np.maximum(self.regs, maxregs).astype(np.uint8)
+
+    @property
+    def sparse_ops(self) -> bytes:
+        return self.ops[:self.len.value].tobytes()
+
+    def string(self, card: bytes) -> bytes:
+        """GET: header (card = the 8 cached-cardinality bytes) + opcodes or dense registers."""
+        if self.dense.value:
+            return b"HYLL" + bytes([0, 0, 0, 0]) + card + hll_dense_pack(self.regs)
+        return b"HYLL" + bytes([1, 0, 0, 0]) + card + self.sparse_ops

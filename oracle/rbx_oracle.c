@@ -570,3 +570,198 @@ void orc_hash128_batch(const uint8_t *bytes, const uint64_t *offsets, uint64_t n
     for (uint64_t i = 0; i < n; i++)
         orc_redisson_hash128(bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), out + 2 * i);
 }
+
+/* ------------------------------------------------------------------------- */
+/* Sparse HLL strings [redis-7.2 src/hyperloglog.c hllSparseSet / hllSparseAdd /  */
+/* pfaddCommand / pfmergeCommand, external -- restated byte for byte].  The caller */
+/* is M/RedissonHyperLogLog.java:71-102 (PFADD / PFMERGE); Redis keeps the sparse   */
+/* string it built incrementally, so GET bytes depend on the order of the updates. */
+/* `ops` is the opcode string without the 16-byte header, *len its length, cap its */
+/* capacity (>= *len + 3).  max_bytes = hll-sparse-max-bytes, compared with the    */
+/* whole string (header included), as sdslen(o->ptr) is.                          */
+/* Returns 0 = no change, 1 = updated, 2 = promote (string untouched), -1 invalid.  */
+/* ------------------------------------------------------------------------- */
+#define SP_IS_ZERO(p) (((*(p)) & 0xc0) == 0)
+#define SP_IS_XZERO(p) (((*(p)) & 0xc0) == 0x40)
+#define SP_IS_VAL(p) ((*(p)) & 0x80)
+#define SP_ZERO_LEN(p) (((*(p)) & 0x3f) + 1)
+#define SP_XZERO_LEN(p) (((((*(p)) & 0x3f) << 8) | (*((p) + 1))) + 1)
+#define SP_VAL_VALUE(p) ((((*(p)) >> 2) & 0x1f) + 1)
+#define SP_VAL_LEN(p) (((*(p)) & 0x3) + 1)
+#define SP_ZERO_SET(p, len) (*(p) = (uint8_t)((len) - 1))
+#define SP_XZERO_SET(p, len)                          \
+    do {                                              \
+        int _l = (len) - 1;                           \
+        *(p) = (uint8_t)((_l >> 8) | 0x40);           \
+        *((p) + 1) = (uint8_t)(_l & 0xff);            \
+    } while (0)
+#define SP_VAL_SET(p, val, len) (*(p) = (uint8_t)((((val) - 1) << 2 | ((len) - 1)) | 0x80))
+
+int orc_hll_sparse_set(uint8_t *ops, size_t *len, size_t cap, long index, int count, size_t max_bytes) {
+    if (count > 32) return 2; /* HLL_SPARSE_VAL_MAX_VALUE */
+    if (cap < *len + 3) return -1;
+    uint8_t *sparse = ops, *p = ops, *end = ops + *len, *prev = NULL, *next;
+    long first = 0, span = 0;
+    /* step 1: the opcode covering `index` */
+    while (p < end) {
+        long oplen = 1;
+        if (SP_IS_ZERO(p)) {
+            span = SP_ZERO_LEN(p);
+        } else if (SP_IS_VAL(p)) {
+            span = SP_VAL_LEN(p);
+        } else {
+            span = SP_XZERO_LEN(p);
+            oplen = 2;
+        }
+        if (index <= first + span - 1) break;
+        prev = p;
+        p += oplen;
+        first += span;
+    }
+    if (span == 0 || p >= end) return -1;
+    next = SP_IS_XZERO(p) ? p + 2 : p + 1;
+    if (next >= end) next = NULL;
+    int is_zero = 0, is_xzero = 0, is_val = 0;
+    long runlen;
+    if (SP_IS_ZERO(p)) {
+        is_zero = 1;
+        runlen = SP_ZERO_LEN(p);
+    } else if (SP_IS_XZERO(p)) {
+        is_xzero = 1;
+        runlen = SP_XZERO_LEN(p);
+    } else {
+        is_val = 1;
+        runlen = SP_VAL_LEN(p);
+    }
+    /* step 2: cases A-C */
+    if (is_val) {
+        if (SP_VAL_VALUE(p) >= count) return 0;
+        if (runlen == 1) {
+            SP_VAL_SET(p, count, 1);
+            goto updated;
+        }
+    }
+    if (is_zero && runlen == 1) {
+        SP_VAL_SET(p, count, 1);
+        goto updated;
+    }
+    /* case D: split into at most three opcodes (<= 5 bytes) */
+    {
+        uint8_t seq[5], *n = seq;
+        long last = first + span - 1, l;
+        if (is_zero || is_xzero) {
+            if (index != first) {
+                l = index - first;
+                if (l > 64) {
+                    SP_XZERO_SET(n, l);
+                    n += 2;
+                } else {
+                    SP_ZERO_SET(n, l);
+                    n++;
+                }
+            }
+            SP_VAL_SET(n, count, 1);
+            n++;
+            if (index != last) {
+                l = last - index;
+                if (l > 64) {
+                    SP_XZERO_SET(n, l);
+                    n += 2;
+                } else {
+                    SP_ZERO_SET(n, l);
+                    n++;
+                }
+            }
+        } else {
+            int curval = SP_VAL_VALUE(p);
+            if (index != first) {
+                l = index - first;
+                SP_VAL_SET(n, curval, l);
+                n++;
+            }
+            SP_VAL_SET(n, count, 1);
+            n++;
+            if (index != last) {
+                l = last - index;
+                SP_VAL_SET(n, curval, l);
+                n++;
+            }
+        }
+        /* step 3: substitute */
+        long seqlen = n - seq, oldlen = is_xzero ? 2 : 1, deltalen = seqlen - oldlen;
+        if (deltalen > 0 && 16 + *len + deltalen > max_bytes) return 2;
+        if (deltalen && next) memmove(next + deltalen, next, (size_t)(end - next));
+        *len += deltalen;
+        memcpy(p, seq, (size_t)seqlen);
+        end += deltalen;
+    }
+updated:
+    /* step 4: merge adjacent VAL opcodes of one value, up to 5 opcodes from prev */
+    p = prev ? prev : sparse;
+    int scanlen = 5;
+    while (p < end && scanlen--) {
+        if (SP_IS_XZERO(p)) {
+            p += 2;
+            continue;
+        } else if (SP_IS_ZERO(p)) {
+            p++;
+            continue;
+        }
+        if (p + 1 < end && SP_IS_VAL(p + 1)) {
+            int v1 = SP_VAL_VALUE(p), v2 = SP_VAL_VALUE(p + 1);
+            if (v1 == v2) {
+                int l = SP_VAL_LEN(p) + SP_VAL_LEN(p + 1);
+                if (l <= 4) {
+                    SP_VAL_SET(p + 1, v1, l);
+                    memmove(p, p + 1, (size_t)(end - p));
+                    *len -= 1;
+                    end--;
+                    continue; /* retry at p: the merged opcode may merge again */
+                }
+            }
+        }
+        p++;
+    }
+    return 1;
+}
+
+/* createHLLObject: one XZERO covering the 16384 registers (2 bytes). */
+size_t orc_hll_sparse_new(uint8_t *ops) {
+    SP_XZERO_SET(ops, HLL_REGISTERS);
+    return 2;
+}
+
+/* PFADD on an HLL held as (regs, sparse string, *dense): elements in order; while sparse each
+ * goes through hllSparseSet, the first promotion converts to dense (the registers are kept in
+ * `regs` throughout).  Returns 1 iff a register changed. */
+int orc_hll_sparse_pfadd(uint8_t *ops, size_t *len, size_t cap, int *dense, uint8_t *regs, const uint8_t *bytes,
+                         const uint64_t *offsets, uint64_t n, size_t max_bytes) {
+    int updated = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        long index;
+        int count = orc_hll_patlen(bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), &index);
+        if (!*dense) {
+            int r = orc_hll_sparse_set(ops, len, cap, index, count, max_bytes);
+            if (r < 0) return -1;
+            if (r == 2) *dense = 1;
+        }
+        if (count > regs[index]) {
+            regs[index] = (uint8_t)count;
+            updated = 1;
+        }
+    }
+    return updated;
+}
+
+/* pfmergeCommand's write-back into a sparse destination: hllSparseSet(j, max[j]) for every
+ * nonzero max[j], ascending j (a promotion converts the rest to dense).  `maxregs` already
+ * includes the destination's own registers. */
+int orc_hll_sparse_merge(uint8_t *ops, size_t *len, size_t cap, int *dense, const uint8_t *maxregs, size_t max_bytes) {
+    for (long j = 0; j < HLL_REGISTERS && !*dense; j++) {
+        if (!maxregs[j]) continue;
+        int r = orc_hll_sparse_set(ops, len, cap, j, maxregs[j], max_bytes);
+        if (r < 0) return -1;
+        if (r == 2) *dense = 1;
+    }
+    return 0;
+}

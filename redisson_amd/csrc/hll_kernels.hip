@@ -194,74 +194,248 @@ void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipSt
 }
 
 // ---------------------------------------------------------------------------------
-// sparse-limit check (one block per HLL): would the registers still fit Redis' sparse string?
-// Bytes of the fewest-bytes opcode form: a zero run costs 1 byte (ZERO, <= 64) or 2 (XZERO), a
-// run of value v <= 32 costs ceil(len / 4) bytes (VAL); a register > 32 forces dense.  Thread t
-// owns registers [64t, 64t + 64); a run is charged by the thread holding its first register,
-// which finds the run's end through a suffix minimum of the threads' first run starts.
+// Sparse strings, replayed ([redis-7.2] hyperloglog.c hllSparseSet, restated in
+// oracle/rbx_oracle.c orc_hll_sparse_set).  Redis updates a sparse HLL element by element: the
+// opcode covering the register is split into at most three (case D), the string may not grow
+// past hll-sparse-max-bytes (else the key is promoted to dense for good), and up to five opcodes
+// from the previous one are scanned to merge adjacent VALs of one value (runs of <= 4).  The
+// bytes it ends with depend on the order of the updates, so they are replayed here, in command
+// order, one block per sparse HLL: the block holds the string as run starts in LDS -- a bitmap
+// of the registers that start an opcode (+ a summary of its nonzero words) and the opcode at
+// each start -- so finding the opcode that covers a register is two or three LDS reads instead
+// of a walk over the string.  The lanes hash 256 elements at a time and mark those that raise
+// their register (count > the value the string holds); lane 0 applies them in element order
+// (the rest cannot change anything: registers only grow).  The registers themselves are
+// updated by k_hll_pfadd / k_hll_merge as for dense keys; this kernel owns only the string
+// and the promotion word.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_hll_sparse_check(const HllCheck *__restrict__ items, uint64_t max_bytes) {
-    const HllCheck it = items[blockIdx.x];
-    __shared__ uint32_t s_first[257];
-    __shared__ uint32_t s_sum[4], s_max[4];
-    if (__hip_atomic_load(it.promoted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // sticky, uniform
-    const uint32_t t = threadIdx.x, base = t * 64;
-    uint8_t r[64];
-    const u8x16 *src = (const u8x16 *)(it.regs + base);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const u8x16 v = src[q];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) r[q * 16 + j] = v[j];
+namespace sp {
+__device__ __forceinline__ bool is_val(uint32_t op) { return op >= 0x80u && op < 0x100u; }
+__device__ __forceinline__ bool is_xzero(uint32_t op) { return op >= 0x100u; }
+__device__ __forceinline__ uint32_t len(uint32_t op) {
+    return op < 0x80u ? op + 1u : (op < 0x100u ? (op & 3u) + 1u : (op & 0x3fffu) + 1u);
+}
+__device__ __forceinline__ uint32_t bytes(uint32_t op) { return op >= 0x100u ? 2u : 1u; }
+__device__ __forceinline__ uint32_t value(uint32_t op) { return ((op >> 2) & 31u) + 1u; }
+__device__ __forceinline__ uint32_t mkval(uint32_t v, uint32_t l) { return 0x80u | ((v - 1u) << 2) | (l - 1u); }
+__device__ __forceinline__ uint32_t mkzero(uint32_t l) { return l > 64u ? (0x4000u | (l - 1u)) : l - 1u; }
+
+struct Lds {
+    unsigned long long bits[256];  // bit r: register r starts an opcode
+    unsigned long long sum[4];     // bit w: bits[w] != 0
+    uint16_t meta[kHllRegs];       // the opcode starting at register r
+    uint32_t idx[256];
+    uint32_t cnt[256];
+    unsigned long long mask[4];    // per wave: elements that raise their register
+    uint32_t part[256];
+    uint32_t nbytes, state, changed;
+};
+
+__device__ __forceinline__ uint32_t pred(const Lds &L, uint32_t r) {  // the start covering r
+    const uint32_t w = r >> 6;
+    const unsigned long long m = L.bits[w] & (~0ULL >> (63u - (r & 63u)));
+    if (m) return (w << 6) + 63u - (uint32_t)__builtin_clzll(m);
+    int sw = (int)(w >> 6);
+    unsigned long long mm = L.sum[sw] & ((1ULL << (w & 63u)) - 1ULL);
+    while (!mm) mm = L.sum[--sw];  // register 0 always starts an opcode
+    const uint32_t w2 = ((uint32_t)sw << 6) + 63u - (uint32_t)__builtin_clzll(mm);
+    return (w2 << 6) + 63u - (uint32_t)__builtin_clzll(L.bits[w2]);
+}
+
+__device__ __forceinline__ void set_start(Lds &L, uint32_t r, uint32_t op) {
+    L.bits[r >> 6] |= 1ULL << (r & 63u);
+    L.sum[r >> 12] |= 1ULL << ((r >> 6) & 63u);
+    L.meta[r] = (uint16_t)op;
+}
+
+__device__ __forceinline__ void clear_start(Lds &L, uint32_t r) {
+    const unsigned long long b = L.bits[r >> 6] & ~(1ULL << (r & 63u));
+    L.bits[r >> 6] = b;
+    if (!b) L.sum[r >> 12] &= ~(1ULL << ((r >> 6) & 63u));
+}
+
+__device__ __forceinline__ uint32_t value_at(const Lds &L, uint32_t r) {
+    const uint32_t op = L.meta[pred(L, r)];
+    return is_val(op) ? value(op) : 0u;
+}
+
+// hllSparseSet on the LDS image (lane 0 only): 0 = no change, 1 = updated, 2 = promote
+__device__ uint32_t set(Lds &L, uint32_t index, uint32_t count, uint64_t max_bytes) {
+    if (count > 32u) return 2u;  // HLL_SPARSE_VAL_MAX_VALUE
+    const uint32_t first = pred(L, index), op = L.meta[first], span = len(op), last = first + span - 1u;
+    if (is_val(op)) {
+        if (value(op) >= count) return 0u;  // case A
+        if (span == 1u) {                   // case B
+            L.meta[first] = (uint16_t)mkval(count, 1u);
+            goto updated;
+        }
+    } else if (!is_xzero(op) && span == 1u) {  // case C
+        L.meta[first] = (uint16_t)mkval(count, 1u);
+        goto updated;
     }
-    const uint32_t prev = t ? it.regs[base - 1] : 0xffffffffu;
-    uint64_t starts = 0;
-    uint32_t vmax = 0;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        const uint32_t p = j ? (uint32_t)r[j - 1] : prev;
-        if (r[j] != p) starts |= 1ULL << j;
-        vmax = r[j] > vmax ? r[j] : vmax;
+    {  // case D: split into <= 3 opcodes
+        uint32_t q[3], qs[3], nq = 0, seq = 0;
+        const bool zero = !is_val(op);
+        const uint32_t cur = zero ? 0u : value(op);
+        if (index != first) {
+            q[nq] = zero ? mkzero(index - first) : mkval(cur, index - first);
+            qs[nq++] = first;
+        }
+        q[nq] = mkval(count, 1u);
+        qs[nq++] = index;
+        if (index != last) {
+            q[nq] = zero ? mkzero(last - index) : mkval(cur, last - index);
+            qs[nq++] = index + 1u;
+        }
+        for (uint32_t i = 0; i < nq; ++i) seq += bytes(q[i]);
+        const int delta = (int)seq - (int)bytes(op);
+        if (delta > 0 && 16u + (uint64_t)L.nbytes + (uint64_t)delta > max_bytes) return 2u;
+        for (uint32_t i = 0; i < nq; ++i) set_start(L, qs[i], q[i]);
+        L.nbytes = (uint32_t)((int)L.nbytes + delta);
     }
-    s_first[t] = starts ? base + (uint32_t)__builtin_ctzll(starts) : 16384u;
-    if (t == 0) s_first[256] = 16384u;
+updated:
+    {  // merge adjacent VALs of one value, scanning up to 5 opcodes from the previous one
+        uint32_t p = first ? pred(L, first - 1u) : 0u;
+        for (int scan = 5; p < (uint32_t)kHllRegs && scan-- > 0;) {
+            const uint32_t o = L.meta[p], nx = p + len(o);
+            if (is_val(o) && nx < (uint32_t)kHllRegs) {
+                const uint32_t o2 = L.meta[nx];
+                if (is_val(o2) && value(o2) == value(o) && len(o) + len(o2) <= 4u) {
+                    L.meta[p] = (uint16_t)mkval(value(o), len(o) + len(o2));
+                    clear_start(L, nx);
+                    L.nbytes -= 1u;
+                    continue;  // the merged opcode may merge again
+                }
+            }
+            p = nx;
+        }
+    }
+    return 1u;
+}
+
+// exclusive block scan of one value per thread (256 threads); returns the total
+__device__ __forceinline__ uint32_t block_scan(Lds &L, uint32_t v, uint32_t &excl) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63u) L.part[wave] = x;
     __syncthreads();
-    // suffix minimum over the threads' first starts (256 entries, in place)
-    for (uint32_t off = 1; off < 256; off <<= 1) {
-        const uint32_t o = t + off < 256 ? s_first[t + off] : 16384u;
-        __syncthreads();
-        s_first[t] = min(s_first[t], o);
-        __syncthreads();
-    }
-    const uint32_t next_after = t + 1 < 256 ? s_first[t + 1] : 16384u;  // first start past my range
-    uint32_t bytes = 0;
-    for (uint64_t m = starts; m; m &= m - 1) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        const uint64_t later = m & (m - 1);
-        const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
-        const uint32_t len = end - (base + j), v = r[j];
-        bytes += v == 0 ? (len > 64 ? 2u : 1u) : (len + 3) / 4;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        bytes += __shfl_down(bytes, off, 64);
-        vmax = max(vmax, (uint32_t)__shfl_down(vmax, off, 64));
-    }
-    if ((t & 63) == 0) {
-        s_sum[t >> 6] = bytes;
-        s_max[t >> 6] = vmax;
-    }
-    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; ++w) base += L.part[w];
+    const uint32_t total = L.part[0] + L.part[1] + L.part[2] + L.part[3];
+    excl = base + x - v;
+    __syncthreads();  // part[] reuse
+    return total;
+}
+}  // namespace sp
+
+template <int ELEN>
+__global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const HllReplay *__restrict__ items,
+                                                           uint64_t max_bytes) {
+    __shared__ sp::Lds L;
+    const HllReplay it = items[blockIdx.x];
+    if (__hip_atomic_load(it.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // promoted: uniform
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    // load: opcode list -> run starts (thread t takes a contiguous slice of the list)
+    const uint32_t nent = min(it.state[1], (uint32_t)kHllRegs);
+    L.bits[t] = 0;
     if (t == 0) {
-        const uint32_t total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-        const uint32_t mx = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
-        if (mx > 32 || 16 + (uint64_t)total > max_bytes) *it.promoted = 1u;
+        L.nbytes = nent ? it.state[2] : 2u;
+        L.state = 0;
+        L.changed = 0;
+    }
+    const uint32_t per = (nent + 255u) / 256u, e0 = min(t * per, nent), e1 = min(e0 + per, nent);
+    uint32_t span = 0;
+    for (uint32_t e = e0; e < e1; ++e) span += sp::len(it.ops[e]);
+    uint32_t start;
+    sp::block_scan(L, span, start);  // (barriers inside order the bits reset)
+    for (uint32_t e = e0; e < e1; ++e) {
+        const uint32_t op = it.ops[e];
+        if (start < (uint32_t)kHllRegs) {
+            atomicOr(&L.bits[start >> 6], 1ULL << (start & 63u));
+            L.meta[start] = (uint16_t)op;
+        }
+        start += sp::len(op);
+    }
+    if (nent == 0 && t == 0) {  // createHLLObject: XZERO over the 16384 registers
+        L.bits[0] = 1ULL;
+        L.meta[0] = 0x7fffu;
+    }
+    __syncthreads();
+    {
+        const unsigned long long nz = __ballot(L.bits[t] != 0ULL);
+        if (lane == 0) L.sum[wave] = nz;
+    }
+    __syncthreads();
+    // updates in order, 256 at a time
+    const bool merge = it.regs != nullptr;
+    const uint64_t b0 = merge ? 0 : it.begin, b1 = merge ? (uint64_t)kHllRegs : it.end;
+    for (uint64_t base = b0; base < b1; base += 256) {
+        const uint64_t e = base + t;
+        bool cand = false;
+        if (e < b1) {
+            uint32_t idx, cnt;
+            if (merge) {
+                idx = (uint32_t)e;
+                cnt = it.regs[e];
+            } else {
+                const uint64_t h = elem_hash<ELEN>(elems, e);
+                idx = (uint32_t)(h & (kHllRegs - 1));
+                cnt = hll_count_of(h);
+            }
+            L.idx[t] = idx;
+            L.cnt[t] = cnt;
+            cand = cnt > sp::value_at(L, idx);
+        }
+        const unsigned long long m = __ballot(cand);
+        if (lane == 0) L.mask[wave] = m;
+        __syncthreads();
+        if (t == 0) {
+            for (uint32_t w = 0; w < 4u && !L.state; ++w) {
+                for (unsigned long long mm = L.mask[w]; mm; mm &= mm - 1) {
+                    const uint32_t i = w * 64u + (uint32_t)__builtin_ctzll(mm);
+                    const uint32_t r = sp::set(L, L.idx[i], L.cnt[i], max_bytes);
+                    if (r == 2u) {
+                        L.state = 1;
+                        break;
+                    }
+                    L.changed |= r;
+                }
+            }
+        }
+        __syncthreads();
+        if (L.state) break;  // uniform
+    }
+    if (L.state) {
+        if (t == 0) it.state[0] = 1u;  // the registers go on in k_hll_pfadd / k_hll_merge
+        return;
+    }
+    if (!L.changed) return;  // uniform
+    // write back: thread t serializes the starts of registers [64t, 64t + 64)
+    const unsigned long long w = L.bits[t];
+    uint32_t pos;
+    const uint32_t total = sp::block_scan(L, (uint32_t)__builtin_popcountll(w), pos);
+    for (unsigned long long m = w; m; m &= m - 1) it.ops[pos++] = L.meta[t * 64u + (uint32_t)__builtin_ctzll(m)];
+    if (t == 0) {
+        it.state[1] = total;
+        it.state[2] = L.nbytes;
     }
 }
 
-void launch_hll_sparse_check(const HllCheck *items, uint32_t n, uint64_t max_bytes, hipStream_t st) {
+void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,
+                              uint64_t max_bytes, hipStream_t st) {
     if (!n) return;
-    hipLaunchKernelGGL(k_hll_sparse_check, dim3(n), dim3(256), 0, st, items, max_bytes);
+    switch (elen_fast) {
+    case 16: hipLaunchKernelGGL(k_hll_sparse_replay<16>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    case 32: hipLaunchKernelGGL(k_hll_sparse_replay<32>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    case 64: hipLaunchKernelGGL(k_hll_sparse_replay<64>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    case 8: hipLaunchKernelGGL(k_hll_sparse_replay<8>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    default: hipLaunchKernelGGL(k_hll_sparse_replay<0>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    }
 }
 
 // ---------------------------------------------------------------------------------

@@ -130,7 +130,10 @@ struct Bitmap {  // a Redis string used with SETBIT/GETBIT
 
 struct HllState {  // a Redis HLL string, registers unpacked (1 byte each) on the device
     uint8_t *d_regs = nullptr;  // 16384 bytes inside a pool chunk
-    uint32_t *d_promoted = nullptr;  // device word: a PFADD made the sparse string exceed its limits
+    // device state words (HllReplay::state): [0] promoted -- a PFADD / PFMERGE promoted the sparse
+    // string to dense --, [1] opcodes in d_sp_ops (0 = the createHLLObject string), [2] its bytes
+    uint32_t *d_promoted = nullptr;
+    uint16_t *d_sp_ops = nullptr;  // the sparse string as Redis built it, one u16 per opcode
     uint64_t card = 0;          // the header's 8 cached-cardinality bytes (LE); bit 63 = invalid
     bool dense = false;         // Redis encoding: created sparse, promoted to dense once (never back)
     struct ::rbx_ctx *owner = nullptr;
@@ -200,9 +203,14 @@ struct rbx_ctx {
 
     // HLL register pool: chunks of kHllPerChunk x 16 KiB
     std::vector<uint8_t *> hll_chunks;
-    std::vector<std::pair<uint8_t *, uint32_t *>> hll_free;  // (registers, promotion word)
-    DevBuf hll_checks;                     // k_hll_sparse_check items (cached by content)
-    std::vector<HllCheck> check_cache;
+    struct HllSlot {
+        uint8_t *regs;
+        uint32_t *state;
+        uint16_t *ops;
+    };
+    std::vector<HllSlot> hll_free;  // (registers, state words, sparse opcodes)
+    DevBuf hll_checks;                     // k_hll_sparse_replay items (cached by content)
+    std::vector<HllReplay> check_cache;
 
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -250,13 +258,15 @@ struct ScratchOrder {
 };
 
 static constexpr size_t kHllBytes = 16384;
-static constexpr size_t kHllPerChunk = 4096;  // 64 MiB per pool chunk
+static constexpr size_t kHllPerChunk = 4096;  // 192 MiB per pool chunk
+static constexpr size_t kHllStateWords = 4;   // HllReplay::state, 16 bytes
+static constexpr size_t kHllOpsBytes = 16384 * 2;  // a sparse string has <= 16384 opcodes
 
 rbx::HllState::~HllState() {
     if (d_regs && owner) {
         {
             std::lock_guard<std::recursive_mutex> g(owner->ks.mu);
-            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted});
+            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted, d_sp_ops});
         }
         ctx_release(owner);
     }
@@ -265,22 +275,26 @@ rbx::HllState::~HllState() {
 // A fresh zeroed HLL register block; the fill runs on `st` (see SlabPool).
 static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out) {
     if (c->hll_free.empty()) {
-        // registers of kHllPerChunk HLLs, then their promotion words
+        // registers of kHllPerChunk HLLs, then their state words, then their sparse opcode lists
         uint8_t *chunk = nullptr;
-        HIP_TRY(hipMalloc(&chunk, (kHllBytes + 4) * kHllPerChunk));
+        HIP_TRY(hipMalloc(&chunk, (kHllBytes + kHllStateWords * 4 + kHllOpsBytes) * kHllPerChunk));
         c->hll_chunks.push_back(chunk);
         uint32_t *words = (uint32_t *)(chunk + kHllBytes * kHllPerChunk);
+        uint16_t *ops = (uint16_t *)(words + kHllStateWords * kHllPerChunk);
         // hand out in reverse so that successive allocations are ascending
-        for (size_t i = kHllPerChunk; i-- > 0;) c->hll_free.push_back({chunk + i * kHllBytes, words + i});
+        for (size_t i = kHllPerChunk; i-- > 0;)
+            c->hll_free.push_back({chunk + i * kHllBytes, words + i * kHllStateWords, ops + i * (kHllOpsBytes / 2)});
     }
     auto h = std::make_shared<HllState>();
-    h->d_regs = c->hll_free.back().first;
-    h->d_promoted = c->hll_free.back().second;
+    h->d_regs = c->hll_free.back().regs;
+    h->d_promoted = c->hll_free.back().state;
+    h->d_sp_ops = c->hll_free.back().ops;
     c->hll_free.pop_back();
     h->owner = c;
     c->refs.fetch_add(1);
     HIP_TRY(hipMemsetAsync(h->d_regs, 0, kHllBytes, st));
-    HIP_TRY(hipMemsetAsync(h->d_promoted, 0, 4, st));
+    // state 0: not promoted, the createHLLObject sparse string (one XZERO)
+    HIP_TRY(hipMemsetAsync(h->d_promoted, 0, kHllStateWords * 4, st));
     *out = h;
     return RBX_OK;
 }
@@ -1652,32 +1666,37 @@ static int hll_bind(rbx_ctx *c, rbx_hll *h, bool create, hipStream_t st) {
     return RBX_OK;
 }
 
-// Redis promotes a sparse HLL to dense (one way) when an update would store a value > 32 or grow
-// the sparse string past hll-sparse-max-bytes ([redis-7.2] hyperloglog.c hllSparseSet).  After
-// every PFADD command (and PFMERGE into a sparse destination) k_hll_sparse_check sets the HLL's
-// sticky device word when its registers no longer fit; RBX_HLL_AS_STORED export and PFMERGE read
-// it.  (Redis checks after every element; the sparse length is not monotone -- runs can merge --
-// so a string that exceeded the limit mid-command and shrank again by its end stays sparse here:
-// parity unpinned without a live redis-server.)
-static int sparse_check(rbx_ctx *c, const std::vector<HllState *> &hl, hipStream_t st) {
-    std::vector<HllCheck> items;
+// Redis keeps a PFADD-created HLL sparse until an update would store a value > 32 or grow the
+// string past hll-sparse-max-bytes, then promotes it to dense for good ([redis-7.2]
+// hyperloglog.c hllSparseSet), and the sparse bytes depend on the order of the updates.
+// k_hll_sparse_replay applies each command's updates, in order, to the sparse HLLs' strings on
+// the device (the registers are updated by the PFADD / merge kernels as for dense keys) and sets
+// the sticky promotion word at the first promotion.  `items` = one per sparse HLL of a round.
+static int replay_sparse(rbx_ctx *c, std::vector<HllReplay> &items, const KeysDev &dk, int fl, hipStream_t st) {
+    if (items.empty()) return RBX_OK;
+    const bool same = c->check_cache.size() == items.size() &&
+                      memcmp(c->check_cache.data(), items.data(), items.size() * sizeof(HllReplay)) == 0;
+    if (!same) {
+        RBX_TRY(c->hll_checks.reserve(items.size() * sizeof(HllReplay)));
+        HIP_TRY(hipMemcpyAsync(c->hll_checks.p, items.data(), items.size() * sizeof(HllReplay), hipMemcpyHostToDevice, st));
+        c->check_cache = items;
+    }
+    launch_hll_sparse_replay(dk, fl, c->hll_checks.as<HllReplay>(), (uint32_t)items.size(), kHllSparseMaxBytes, st);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
+// PFMERGE-style write-back (ascending registers) of the sparse HLLs among hl; their registers
+// already hold the merged maxima
+static int replay_merge(rbx_ctx *c, const std::vector<HllState *> &hl, hipStream_t st) {
+    std::vector<HllReplay> items;
     std::unordered_map<HllState *, int> seen;
     for (HllState *h : hl)
         if (h && !h->dense && !seen.count(h)) {
             seen[h] = 1;
-            items.push_back(HllCheck{h->d_regs, h->d_promoted});
+            items.push_back(HllReplay{h->d_sp_ops, h->d_promoted, h->d_regs, 0, 0});
         }
-    if (items.empty()) return RBX_OK;
-    const bool same = c->check_cache.size() == items.size() &&
-                      memcmp(c->check_cache.data(), items.data(), items.size() * sizeof(HllCheck)) == 0;
-    if (!same) {
-        RBX_TRY(c->hll_checks.reserve(items.size() * sizeof(HllCheck)));
-        HIP_TRY(hipMemcpyAsync(c->hll_checks.p, items.data(), items.size() * sizeof(HllCheck), hipMemcpyHostToDevice, st));
-        c->check_cache = items;
-    }
-    launch_hll_sparse_check(c->hll_checks.as<HllCheck>(), (uint32_t)items.size(), kHllSparseMaxBytes, st);
-    HIP_TRY(hipGetLastError());
-    return RBX_OK;
+    return replay_sparse(c, items, KeysDev{}, 0, st);
 }
 
 // host view of the promotion word (the caller holds a ScratchOrder on c->stream)
@@ -1723,8 +1742,11 @@ static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64
             }
             launch_hll_pfadd(dk, fl, c->hll_tiles.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
             HIP_TRY(hipGetLastError());
-            std::vector<HllState *> round(hl.begin() + s0, hl.begin() + s1);
-            RBX_TRY(sparse_check(c, round, st));
+            std::vector<HllReplay> items;  // the round's HLLs are distinct
+            for (uint32_t s = s0; s < s1; ++s)
+                if (!hl[s]->dense && h_seg[s + 1] > h_seg[s])
+                    items.push_back(HllReplay{hl[s]->d_sp_ops, hl[s]->d_promoted, nullptr, h_seg[s], h_seg[s + 1]});
+            RBX_TRY(replay_sparse(c, items, dk, fl, st));
         }
         s0 = s1;
     }
@@ -2002,7 +2024,7 @@ static int hll_merge(rbx_ctx *c, const std::string &dest, const std::vector<std:
         HIP_TRY(hipMemcpyAsync(c->ptrs.p, sp.data(), sp.size() * sizeof(uint8_t *), hipMemcpyHostToDevice, c->stream));
         launch_hll_merge(d->d_regs, c->ptrs.as<uint8_t *>(), (uint32_t)sp.size(), c->stream);
         HIP_TRY(hipGetLastError());
-        RBX_TRY(sparse_check(c, {d.get()}, c->stream));
+        RBX_TRY(replay_merge(c, {d.get()}, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
@@ -2045,9 +2067,8 @@ static void hll_encode_dense(const uint8_t *regs, uint8_t *p) {
 
 // Sparse opcodes with the fewest bytes: zero runs as ZERO (<= 64) or XZERO (65..16384), equal
 // values as VAL runs of <= 4 (value 1..32).  Returns false when a register exceeds 32 (the
-// sparse format cannot hold it).  Redis builds its sparse string incrementally (hllSparseSet);
-// zero runs come out identical, runs of one value may be split differently (4+1 vs 1+4), with
-// the same registers.
+// sparse format cannot hold it).  Used for RBX_HLL_SPARSE exports of keys Redis holds dense
+// (a sparse key exports the string it was built as, see hll_sparse_string).
 static bool hll_encode_sparse(const uint8_t *regs, std::vector<uint8_t> &out) {
     out.clear();
     for (uint32_t i = 0; i < 16384;) {
@@ -2072,6 +2093,27 @@ static bool hll_encode_sparse(const uint8_t *regs, std::vector<uint8_t> &out) {
     return true;
 }
 
+// The sparse string of a key Redis holds sparse, as it was built (k_hll_sparse_replay's list):
+// an XZERO opcode is two bytes, ZERO / VAL one.  The caller holds a ScratchOrder on c->stream.
+static int hll_sparse_string(rbx_ctx *c, HllState *h, std::vector<uint8_t> &out) {
+    uint32_t st[kHllStateWords];
+    HIP_TRY(hipMemcpyAsync(st, h->d_promoted, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    out.clear();
+    if (st[1] == 0) {  // createHLLObject
+        out = {0x7f, 0xff};
+        return RBX_OK;
+    }
+    std::vector<uint16_t> ops(st[1]);
+    HIP_TRY(hipMemcpy(ops.data(), h->d_sp_ops, ops.size() * 2, hipMemcpyDeviceToHost));
+    for (uint16_t op : ops) {
+        if (op >= 0x100) out.push_back((uint8_t)(op >> 8));
+        out.push_back((uint8_t)op);
+    }
+    if (out.size() != st[2]) return fail(RBX_E_DEVICE, "sparse HLL string length mismatch");
+    return RBX_OK;
+}
+
 static int hll_export_enc(rbx_ctx *c, const std::string &name, int encoding, uint8_t *out, uint64_t cap,
                           uint64_t *len) {
     if (encoding < RBX_HLL_DENSE || encoding > RBX_HLL_AS_STORED)
@@ -2085,29 +2127,30 @@ static int hll_export_enc(rbx_ctx *c, const std::string &name, int encoding, uin
         if (len) *len = 0;
         return RBX_OK;
     }
-    if (encoding == RBX_HLL_AS_STORED) RBX_TRY(resolve_dense(c, h.get()));
-    std::vector<uint8_t> regs(kHllBytes);
-    HIP_TRY(hipMemcpyAsync(regs.data(), h->d_regs, kHllBytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (encoding != RBX_HLL_DENSE) RBX_TRY(resolve_dense(c, h.get()));
     std::vector<uint8_t> s;
     bool sparse = false;
-    if (encoding == RBX_HLL_SPARSE || (encoding == RBX_HLL_AS_STORED && !h->dense)) {
+    if (encoding != RBX_HLL_DENSE && !h->dense) {
         std::vector<uint8_t> ops;
-        const bool fits = hll_encode_sparse(regs.data(), ops);
-        if (encoding == RBX_HLL_SPARSE && !fits)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "a register exceeds 32: not representable in the sparse encoding");
-        // hllSparseSet promotes once a value exceeds 32 or the string exceeds hll-sparse-max-bytes
-        if (fits && (encoding == RBX_HLL_SPARSE || 16 + ops.size() <= kHllSparseMaxBytes)) {
+        RBX_TRY(hll_sparse_string(c, h.get(), ops));
+        s.resize(16 + ops.size());
+        memcpy(s.data() + 16, ops.data(), ops.size());
+        sparse = true;
+    } else {
+        std::vector<uint8_t> regs(kHllBytes);
+        HIP_TRY(hipMemcpyAsync(regs.data(), h->d_regs, kHllBytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (encoding == RBX_HLL_SPARSE) {
+            std::vector<uint8_t> ops;
+            if (!hll_encode_sparse(regs.data(), ops))
+                return fail(RBX_E_ILLEGAL_ARGUMENT, "a register exceeds 32: not representable in the sparse encoding");
             s.resize(16 + ops.size());
             memcpy(s.data() + 16, ops.data(), ops.size());
             sparse = true;
         } else {
-            h->dense = true;  // promotion is one-way
+            s.resize(kHllDenseLen);
+            hll_encode_dense(regs.data(), s.data() + 16);
         }
-    }
-    if (!sparse) {
-        s.resize(kHllDenseLen);
-        hll_encode_dense(regs.data(), s.data() + 16);
     }
     hll_header(s.data(), sparse, h->card);
     if (len) *len = s.size();
@@ -2133,6 +2176,7 @@ int rbx_hll_export(rbx_ctx *c, const char *name, uint8_t *out, uint64_t cap, uin
 static int hll_import(rbx_ctx *c, const std::string &name, const uint8_t *bytes, uint64_t len) {
     if (len < 16 || memcmp(bytes, "HYLL", 4) != 0 || bytes[4] > 1) return fail(RBX_E_WRONGTYPE, kHllWrongType);
     std::vector<uint8_t> regs(kHllBytes, 0);
+    std::vector<uint16_t> ops;  // sparse: the opcodes as stored (SET keeps the string)
     if (bytes[4] == 0) {
         if (len != kHllDenseLen) return fail(RBX_E_WRONGTYPE, kHllWrongType);
         const uint8_t *p = bytes + 16;
@@ -2149,12 +2193,15 @@ static int hll_import(rbx_ctx *c, const std::string &name, const uint8_t *bytes,
             uint64_t run;
             if ((b & 0xc0) == 0) {  // ZERO
                 run = (b & 0x3f) + 1;
+                ops.push_back(b);
                 p++;
             } else if ((b & 0xc0) == 0x40) {  // XZERO
                 if (p + 1 >= end) return fail(RBX_E_WRONGTYPE, kHllWrongType);
                 run = (((uint64_t)(b & 0x3f) << 8) | p[1]) + 1;
+                ops.push_back((uint16_t)(b << 8 | p[1]));
                 p += 2;
             } else {  // VAL
+                ops.push_back(b);
                 run = (b & 3) + 1;
                 uint8_t v = ((b >> 2) & 0x1f) + 1;
                 if (idx + run > 16384) return fail(RBX_E_WRONGTYPE, kHllWrongType);
@@ -2183,7 +2230,11 @@ static int hll_import(rbx_ctx *c, const std::string &name, const uint8_t *bytes,
     for (int i = 0; i < 8; ++i) card |= (uint64_t)bytes[8 + i] << (8 * i);
     h->card = card;
     h->dense = bytes[4] == 0;  // SET keeps the string's encoding
-    HIP_TRY(hipMemsetAsync(h->d_promoted, 0, 4, c->stream));
+    // state: not promoted, the stored opcodes (a sparse string covers 16384 registers: >= 1)
+    const uint32_t st[kHllStateWords] = {0u, (uint32_t)ops.size(), (uint32_t)(len - 16), 0u};
+    HIP_TRY(hipMemcpyAsync(h->d_promoted, st, sizeof(st), hipMemcpyHostToDevice, c->stream));
+    if (!ops.empty())
+        HIP_TRY(hipMemcpyAsync(h->d_sp_ops, ops.data(), ops.size() * 2, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(h->d_regs, regs.data(), kHllBytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RBX_OK;
@@ -2310,8 +2361,16 @@ static int hll_pack_locked(rbx_ctx *c, rbx_hll *const *hlls, uint32_t n, uint8_t
     HIP_TRY(hipMemcpyAsync(c->ptrs.p, regs.data(), n * sizeof(uint8_t *), hipMemcpyHostToDevice, st));
     launch_hll_pack(c->ptrs.as<uint8_t *>(), n, d_buf, unpack_max, st);
     HIP_TRY(hipGetLastError());
-    if (unpack_max)
-        for (uint32_t i = 0; i < n; ++i) hlls[i]->st->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+    if (unpack_max) {
+        // the exchange merges the other ranks' registers in: a sparse HLL's string takes them
+        // as PFMERGE's write-back would (ascending registers, promotion by the same rules)
+        std::vector<HllState *> hs(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            hlls[i]->st->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+            hs[i] = hlls[i]->st.get();
+        }
+        RBX_TRY(replay_merge(c, hs, st));
+    }
     // `regs` is a pageable host vector: the runtime has staged it when hipMemcpyAsync returns
     return RBX_OK;
 }
@@ -2848,7 +2907,8 @@ int rbx_hll_copy_to(rbx_ctx *src, rbx_name src_name, rbx_ctx *dst, rbx_name dst_
     h->card = sh->card;
     h->dense = sh->dense;
     HIP_TRY(hipMemcpyPeerAsync(h->d_regs, dst->device, sh->d_regs, src->device, kHllBytes, dst->stream));
-    HIP_TRY(hipMemcpyPeerAsync(h->d_promoted, dst->device, sh->d_promoted, src->device, 4, dst->stream));
+    HIP_TRY(hipMemcpyPeerAsync(h->d_promoted, dst->device, sh->d_promoted, src->device, kHllStateWords * 4, dst->stream));
+    HIP_TRY(hipMemcpyPeerAsync(h->d_sp_ops, dst->device, sh->d_sp_ops, src->device, kHllOpsBytes, dst->stream));
     HIP_TRY(hipStreamSynchronize(dst->stream));
     return RBX_OK;
 }

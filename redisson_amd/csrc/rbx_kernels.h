@@ -221,12 +221,19 @@ void launch_hll_count(uint8_t *const *d_regs, uint32_t n, int *d_histo, unsigned
 void launch_hll_merge(uint8_t *dst, uint8_t *const *d_srcs, uint32_t nsrc, hipStream_t st);
 // raw registers -> scratch union: out = max over a set of HLLs (multi-key PFCOUNT)
 void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipStream_t st);
-struct HllCheck {
-    uint8_t *regs;
-    uint32_t *promoted;  // sticky: set when the registers no longer fit a sparse string
+// Redis sparse HLL strings kept as redis-server builds them ([redis-7.2] hyperloglog.c
+// hllSparseSet, replayed in command order): one u16 per opcode -- ZERO and VAL opcodes are their
+// byte, XZERO is (byte0 << 8 | byte1) -- so ZERO < 0x40 <= VAL < 0x100 <= XZERO.
+struct HllReplay {
+    uint16_t *ops;        // the HLL's opcode list (16384 entries of capacity)
+    uint32_t *state;      // [0] promoted (sticky: the list is stale once set), [1] opcodes (0 = the
+                          // createHLLObject string, one XZERO), [2] opcode bytes (after the header)
+    const uint8_t *regs;  // merge mode (PFMERGE write-back): the max registers, ascending; else null
+    uint64_t begin, end;  // PFADD mode: the command's elements, in order
 };
-// per item: promoted |= (a register > 32 || 16 + sparse opcode bytes > max_bytes)
-void launch_hll_sparse_check(const HllCheck *items, uint32_t n, uint64_t max_bytes, hipStream_t st);
+// one block per item; items whose HLL is already promoted return at once
+void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,
+                              uint64_t max_bytes, hipStream_t st);
 // buf[i*16384..] = regs[i] (pack) or regs[i] = max(regs[i], buf[i*16384..]) (unpack_max)
 void launch_hll_pack(uint8_t *const *d_regs, uint32_t n, uint8_t *buf, bool unpack_max, hipStream_t st);
 

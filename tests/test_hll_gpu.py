@@ -214,50 +214,126 @@ def _header(sparse: int, card: bytes) -> bytes:
 
 
 def test_export_sparse_as_stored(client, fresh):
-    """PFADD creates sparse strings ([redis-7.2] createHLLObject); GET returns sparse opcodes
-    until a promotion rule fires.  Byte parity with the oracle's fewest-bytes encoding; Redis'
-    incremental hllSparseSet can split runs of one value differently (same registers)."""
+    """PFADD creates sparse strings ([redis-7.2] createHLLObject); GET returns the sparse string
+    as Redis built it, element by element (hllSparseSet, restated in oracle RedisHll)."""
     rng = np.random.default_rng(11)
     mat = rng.integers(0, 256, size=(300, 16), dtype=np.uint8)
-    regs = O.hll_new()
-    O.hll_pfadd(regs, *O.fixed_arena(mat))
+    ref = O.RedisHll()
+    ref.pfadd(*O.fixed_arena(mat))
     h = client.getHyperLogLog(fresh)
     h.addAll(Arena([bytes(r) for r in mat]))
     s = h.exportString()
-    ops = O.hll_sparse_pack(regs)
-    assert s == _header(1, h.exportDense()[8:16]) + ops
-    assert h.exportString("sparse") == s
-    assert np.array_equal(O.hll_sparse_unpack(s[16:]), regs)
+    assert s == ref.string(h.exportDense()[8:16])
+    assert s[4] == 1 and h.exportString("sparse") == s
+    assert np.array_equal(O.hll_sparse_unpack(s[16:]), ref.regs)
     # SET of the exported string round-trips (and keeps the sparse encoding)
     g = client.getHyperLogLog(fresh + "c")
     g.importString(s)
-    assert g.exportString() == s and np.array_equal(regs_of(g), regs)
-    assert g.count() == h.count() == O.hll_count(regs)
+    assert g.exportString() == s and np.array_equal(regs_of(g), ref.regs)
+    assert g.count() == h.count() == O.hll_count(ref.regs)
     g.delete()
     h.delete()
     assert h.exportString() == b""
 
 
+def test_sparse_string_depends_on_update_order(client, fresh):
+    """Registers 4, 3, 2, 1, 0 raised to 1 in that order: Redis' string is VAL(1,1) VAL(1,4)
+    XZERO -- the merge scan after the last update cannot join a run of 5 -- where the fewest-bytes
+    form of the same registers is VAL(1,4) VAL(1,1) XZERO.  Ascending order gives the latter."""
+    rng = np.random.default_rng(62)
+    els = _count1_elements(range(5), rng)  # sorted by register
+    h = client.getHyperLogLog(fresh)
+    h.addAll(Arena(els[::-1]))
+    s = h.exportString()
+    assert s[16:] == bytes([0x80, 0x83, 0x7F, 0xFA])
+    ref = O.RedisHll()
+    ref.pfadd(*O.arena(els[::-1]))
+    assert s == ref.string(s[8:16])
+    g = client.getHyperLogLog(fresh + "a")
+    g.addAll(Arena(els))
+    assert g.exportString()[16:] == bytes([0x83, 0x80, 0x7F, 0xFA]) == O.hll_sparse_pack(ref.regs)
+    h.delete()
+    g.delete()
+
+
 def test_sparse_promotion_at_max_bytes(client, fresh):
-    """Promotion to dense once the string would exceed hll-sparse-max-bytes (3000), one way."""
+    """Promotion to dense inside the PFADD whose element first grows the string past
+    hll-sparse-max-bytes (3000), one way; every intermediate GET equals Redis' bytes."""
     rng = np.random.default_rng(12)
     h = client.getHyperLogLog(fresh)
-    regs = O.hll_new()
+    ref = O.RedisHll()
     crossed = False
     for _ in range(40):
         mat = rng.integers(0, 256, size=(100, 16), dtype=np.uint8)
-        h.addAll(Arena([bytes(r) for r in mat]))
-        O.hll_pfadd(regs, *O.fixed_arena(mat))
-        ops = O.hll_sparse_pack(regs)
+        assert bool(h.addAll(Arena([bytes(r) for r in mat]))) == bool(ref.pfadd(*O.fixed_arena(mat)))
         s = h.exportString()
-        if ops is not None and 16 + len(ops) <= 3000 and not crossed:
-            assert s[4] == 1 and s[16:] == ops
-        else:
-            crossed = True
-            assert s[4] == 0 and len(s) == 12304 and np.array_equal(O.hll_dense_unpack(s[16:]), regs)
+        assert s == ref.string(s[8:16])
+        crossed = crossed or s[4] == 0
+        if crossed:
+            assert s[4] == 0 and len(s) == 12304
     assert crossed
     assert h.exportString("dense") == h.exportDense()
     h.delete()
+
+
+def test_sparse_strings_batched_commands(client, fresh):
+    """Multi-key PFADD batches (a key may appear several times: successive rounds) over keys
+    that stay sparse, cross the limit mid-command, or start from a SET (non-canonical) string;
+    GET bytes equal the Redis restatement after every batch."""
+    rng = np.random.default_rng(63)
+    keys = [f"{fresh}-{i}" for i in range(6)]
+    refs = {k: O.RedisHll() for k in keys}
+    # key 5 starts as a SET sparse string with unmerged VALs of one value (Redis keeps it as is)
+    raw = bytes([0x84, 0x84, 0x84]) + bytes([0x40 | (16379 >> 8), 16379 & 0xFF]) + bytes([0x80])  # 3 + 16380 + 1
+    s5 = _header(1, bytes(7) + b"\x80") + raw
+    client.getHyperLogLog(keys[5]).importString(s5)
+    refs[keys[5]] = O.RedisHll.from_string(s5)
+    for batch in range(6):
+        names, els = [], []
+        for _ in range(9):
+            k = keys[int(rng.integers(0, len(keys)))]
+            n = int(rng.integers(0, 3 if k == keys[0] else 600))
+            names.append(k)
+            els.append(rng.integers(0, 256, size=(n, 16), dtype=np.uint8))
+        segs = np.zeros(len(names) + 1, np.uint64)
+        segs[1:] = np.cumsum([len(e) for e in els])
+        if not segs[-1]:
+            continue
+        mat = np.concatenate(els)
+        replies = hll_add_multi(client, names, segs, Arena.fixed(mat))
+        for i, (k, e) in enumerate(zip(names, els)):
+            assert bool(replies[i]) == bool(refs[k].pfadd(*O.fixed_arena(e))) or len(e) == 0
+        for k in keys:
+            h = client.getHyperLogLog(k)
+            s = h.exportString()
+            if s:
+                assert s == refs[k].string(s[8:16]), (batch, k)
+    for k in keys:
+        client.getHyperLogLog(k).delete()
+
+
+def test_sparse_merge_write_back_order(client, fresh):
+    """PFMERGE into a sparse destination from sparse sources sets the maxima register by
+    register, ascending (pfmergeCommand), through hllSparseSet -- runs split and merge as in
+    Redis, and the destination promotes if the string outgrows the limit on the way."""
+    rng = np.random.default_rng(64)
+    d = client.getHyperLogLog(fresh + "d")
+    ref = O.RedisHll()
+    e0 = rng.integers(0, 256, size=(40, 16), dtype=np.uint8)
+    d.addAll(Arena([bytes(x) for x in e0]))
+    ref.pfadd(*O.fixed_arena(e0))
+    for i, n in enumerate((30, 200, 500, 900)):
+        src = client.getHyperLogLog(f"{fresh}s{i}")
+        e = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+        src.addAll(Arena([bytes(x) for x in e]))
+        r = O.RedisHll()
+        r.pfadd(*O.fixed_arena(e))
+        d.mergeWith(f"{fresh}s{i}")
+        ref.merge_from(np.maximum(ref.regs, r.regs), use_dense=bool(r.dense.value))
+        s = d.exportString()
+        assert s == ref.string(s[8:16]), i
+        src.delete()
+    d.delete()
 
 
 def test_sparse_export_limits_and_merge_encoding(client, fresh):

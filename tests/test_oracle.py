@@ -175,6 +175,82 @@ def test_hll_sparse_pack_opcodes():
         assert np.array_equal(O.hll_sparse_unpack(O.hll_sparse_pack(r)), r)
 
 
+def _sp_set(ops, n, index, count, max_bytes=3000):
+    import ctypes as C
+    ln = C.c_size_t(n)
+    r = O.lib().orc_hll_sparse_set(O._p(ops), C.byref(ln), ops.size, index, count, max_bytes)
+    return r, ln.value
+
+
+def test_hll_sparse_set_known_answers():
+    """hllSparseSet restatement [redis-7.2 hyperloglog.c, external; parity unpinned: no live
+    redis-server here] on hand-derived cases: case D splits of XZERO / ZERO / VAL, cases A-C,
+    the VAL merge scan, promotion on count > 32 and on hll-sparse-max-bytes."""
+    def fresh():
+        ops = np.zeros(20000, np.uint8)
+        return ops, O.lib().orc_hll_sparse_new(O._p(ops))
+
+    ops, n = fresh()
+    assert ops[:n].tobytes() == b"\x7f\xff"
+    r, n = _sp_set(ops, n, 100, 3)  # XZERO -> XZERO(100) VAL(3,1) XZERO(16283)
+    assert r == 1 and ops[:n].tobytes() == bytes([0x40, 99, 0x88, 0x40 | (16282 >> 8), 16282 & 0xFF])
+    r, n = _sp_set(ops, n, 10, 1)  # XZERO(100) -> ZERO(10) VAL(1,1) XZERO(89): 89 > 64
+    assert r == 1 and ops[:5].tobytes() == bytes([9, 0x80, 0x40, 88, 0x88])
+    assert _sp_set(ops, n, 100, 2) == (0, n)  # case A: VAL 3 >= 2
+    r, n = _sp_set(ops, n, 100, 5)  # case B: VAL len 1 raised in place
+    assert r == 1 and ops[4] == 0x80 | (4 << 2)
+    assert _sp_set(ops, n, 7, 33)[0] == 2  # count > 32: promote
+    # descending 4..0 -> VAL(1,1) VAL(1,4) XZERO; ascending -> VAL(1,4) VAL(1,1) XZERO
+    ops, n = fresh()
+    for i in (4, 3, 2, 1, 0):
+        r, n = _sp_set(ops, n, i, 1)
+    assert ops[:n].tobytes() == bytes([0x80, 0x83, 0x7F, 0xFA])
+    ops, n = fresh()
+    for i in (0, 1, 2, 3, 4):
+        r, n = _sp_set(ops, n, i, 1)
+    assert ops[:n].tobytes() == bytes([0x83, 0x80, 0x7F, 0xFA])
+    # VAL split: VAL(2,4) at 0..3, raise register 1 -> VAL(2,1) VAL(5,1) VAL(2,2)
+    ops, n = fresh()
+    for i in range(4):
+        r, n = _sp_set(ops, n, i, 2)
+    assert ops[:n].tobytes() == bytes([0x87, 0x7F, 0xFB])
+    r, n = _sp_set(ops, n, 1, 5)
+    assert ops[:n].tobytes() == bytes([0x84, 0x90, 0x85, 0x7F, 0xFB])
+    # the size limit: every even register set costs 2 bytes; the update that would pass 3000
+    # returns 2 and leaves the string as it was
+    ops, n = fresh()
+    j = 0
+    while True:
+        before = ops[:n].tobytes()
+        r, n2 = _sp_set(ops, n, j, 1)
+        if r == 2:
+            assert n2 == n and ops[:n].tobytes() == before and 16 + n + 2 > 3000
+            break
+        assert r == 1 and 16 + n2 <= 3000
+        n, j = n2, j + 2
+    assert j > 1000
+
+
+def test_redis_hll_model_invariants():
+    """RedisHll (PFADD element by element): while sparse the string decodes to the registers and
+    fits hll-sparse-max-bytes; the registers equal the order-free PFADD; promotion is one way."""
+    rng = np.random.default_rng(65)
+    h = O.RedisHll()
+    regs = O.hll_new()
+    was_dense = False
+    for _ in range(30):
+        e = rng.integers(0, 256, size=(int(rng.integers(1, 150)), 16), dtype=np.uint8)
+        h.pfadd(*O.fixed_arena(e))
+        O.hll_pfadd(regs, *O.fixed_arena(e))
+        assert np.array_equal(h.regs, regs)
+        if h.dense.value:
+            was_dense = True
+        else:
+            assert not was_dense
+            assert np.array_equal(O.hll_sparse_unpack(h.sparse_ops), regs) and 16 + h.len.value <= 3000
+    assert was_dense
+
+
 def test_multithreaded_restatement_matches_single_thread():
     """rbx_oracle_mt.c (bench.py's all-core cpu_baseline) == rbx_oracle.c, per key and bitmap."""
     rng = np.random.default_rng(31)

@@ -295,6 +295,40 @@ def main():
         h.close()
         fb.delete()
 
+    if "hllfirst" in a.what:
+        # C4-shaped PFADD batch into fresh HLLs (created sparse: the string replay runs until each
+        # promotes) vs the same batch again (dense keys), 10k HLLs x `per` 16-byte elements
+        import ctypes as C
+
+        import numpy as np
+
+        NH = 10_000
+        for per in (1_000, 10_000):
+            hs = []
+            for i in range(NH):
+                hp = C.c_void_p()
+                assert L.lib().rbx_hll_open(client.ctx, f"hf-{per}-{i}".encode(), 1, C.byref(hp)) == 0
+                hs.append(hp.value)
+            arr = (C.c_void_p * NH)(*hs)
+            seg = np.arange(NH + 1, dtype=np.uint64) * np.uint64(per)
+            el = torch.randint(0, 256, (NH * per, 16), dtype=torch.uint8, device="cuda")
+            changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
+            dk = device_keys(el.data_ptr(), NH * per, 16)
+            res = []
+            for _ in range(3):
+                res.append(timed(stream, lambda: L.lib().rbx_hll_add_multi_dev(
+                    client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk), changed.data_ptr(), sp), 1))
+            buf = np.zeros(16 + 12288, np.uint8)
+            ln = C.c_uint64()
+            assert L.lib().rbx_hll_export_enc(client.ctx, f"hf-{per}-0".encode(), 2, buf.ctypes.data_as(L.u8p),
+                                              buf.size, C.byref(ln)) == 0
+            print(json.dumps({"bench": "hllfirst", "hlls": NH, "per": per, "first_ms": res[0], "again_ms": res[1:],
+                              "hll0_encoding": "sparse" if buf[4] else "dense", "hll0_bytes": int(ln.value)}),
+                  flush=True)
+            for hp in hs:
+                L.lib().rbx_hll_close(C.c_void_p(hp))
+            del el
+
     if "addab" in a.what:
         # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
         # round, fresh filter per run: RBX_ADDAB="key=v,key=v;key=v" ("-" = defaults)
