@@ -271,11 +271,15 @@ int rbx_hll_merge(rbx_ctx *ctx, const char *dest, const char *const *srcs, uint3
 int rbx_hll_export(rbx_ctx *ctx, const char *name, uint8_t *out, uint64_t cap, uint64_t *len);
 /* GET name in a chosen encoding ([redis-7.2] hyperloglog.c):
  *   RBX_HLL_DENSE      the dense string (as rbx_hll_export);
- *   RBX_HLL_SPARSE     ZERO / XZERO / VAL opcodes, fewest bytes; ILLEGAL_ARGUMENT if a register > 32;
- *   RBX_HLL_AS_STORED  the encoding Redis would hold: PFADD creates sparse strings, promoted to
- *                      dense (one way) when a register exceeds 32 or the string would exceed
- *                      hll-sparse-max-bytes (3000); SET keeps the imported encoding; PFMERGE's
- *                      destination is dense iff it or any source is.
+ *   RBX_HLL_SPARSE     ZERO / XZERO / VAL opcodes: a key Redis holds sparse exports its string
+ *                      (below); a dense key the fewest-bytes opcodes of its registers
+ *                      (ILLEGAL_ARGUMENT if a register > 32);
+ *   RBX_HLL_AS_STORED  what GET returns in Redis: PFADD creates sparse strings and applies each
+ *                      element in order through hllSparseSet, promoting to dense (one way) at the
+ *                      first element that stores a value > 32 or grows the string past
+ *                      hll-sparse-max-bytes (3000); SET keeps the imported string; PFMERGE's
+ *                      destination is dense iff it or any source is, else its string takes the
+ *                      maxima register by register (pfmergeCommand).
  * *len receives the full length; at most cap bytes are copied. */
 enum { RBX_HLL_DENSE = 0, RBX_HLL_SPARSE = 1, RBX_HLL_AS_STORED = 2 };
 int rbx_hll_export_enc(rbx_ctx *ctx, const char *name, int encoding, uint8_t *out, uint64_t cap, uint64_t *len);
