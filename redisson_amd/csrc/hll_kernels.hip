@@ -334,10 +334,7 @@ __device__ __forceinline__ uint32_t block_scan(Lds &L, uint32_t v, uint32_t &exc
 }  // namespace sp
 
 template <int ELEN>
-__global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const HllReplay *__restrict__ items,
-                                                           uint64_t max_bytes) {
-    __shared__ sp::Lds L;
-    const HllReplay it = items[blockIdx.x];
+__device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems, uint64_t max_bytes) {
     if (__hip_atomic_load(it.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // promoted: uniform
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     // load: opcode list -> run starts (thread t takes a contiguous slice of the list)
@@ -426,15 +423,28 @@ __global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const 
     }
 }
 
+// a grid of <= 2048 blocks walks the items: a steady PFADD stream into keys that have been
+// promoted (the host learns promotions lazily) costs one state load per key, not one block
+template <int ELEN>
+__global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const HllReplay *__restrict__ items,
+                                                           uint32_t n, uint64_t max_bytes) {
+    __shared__ sp::Lds L;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        replay_one<ELEN>(L, items[i], elems, max_bytes);
+        __syncthreads();  // L reuse
+    }
+}
+
 void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,
                               uint64_t max_bytes, hipStream_t st) {
     if (!n) return;
+    const dim3 grid(std::min<uint32_t>(n, 2048));
     switch (elen_fast) {
-    case 16: hipLaunchKernelGGL(k_hll_sparse_replay<16>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
-    case 32: hipLaunchKernelGGL(k_hll_sparse_replay<32>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
-    case 64: hipLaunchKernelGGL(k_hll_sparse_replay<64>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
-    case 8: hipLaunchKernelGGL(k_hll_sparse_replay<8>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
-    default: hipLaunchKernelGGL(k_hll_sparse_replay<0>, dim3(n), dim3(256), 0, st, elems, items, max_bytes); break;
+    case 16: hipLaunchKernelGGL(k_hll_sparse_replay<16>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
+    case 32: hipLaunchKernelGGL(k_hll_sparse_replay<32>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
+    case 64: hipLaunchKernelGGL(k_hll_sparse_replay<64>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
+    case 8: hipLaunchKernelGGL(k_hll_sparse_replay<8>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
+    default: hipLaunchKernelGGL(k_hll_sparse_replay<0>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
     }
 }
 
