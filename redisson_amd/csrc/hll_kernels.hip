@@ -333,9 +333,76 @@ __device__ __forceinline__ uint32_t block_scan(Lds &L, uint32_t v, uint32_t &exc
 }
 }  // namespace sp
 
+// A sufficient condition for a promotion inside the update: the final registers hold a value
+// > 32, or even their fewest-bytes sparse form exceeds the limit while the string started within
+// it.  (Without a promotion every growth of the string was checked, so the final string would fit
+// -- and no encoding of the final registers is shorter than the fewest-bytes one.)  Then the replay is skipped: a large batch
+// into fresh keys costs a register scan, not an element-by-element walk.  Thread t scans
+// registers [64t, 64t + 64); a run is charged by the thread holding its first register, which
+// finds the run's end through a suffix minimum of the threads' first run starts.
+__device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes) {
+    typedef unsigned char u8x16v __attribute__((ext_vector_type(16)));
+    const uint32_t t = threadIdx.x, base = t * 64;
+    uint8_t r[64];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const u8x16v v = ((const u8x16v *)(regs + base))[q];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r[q * 16 + j] = v[j];
+    }
+    const uint32_t prev = t ? regs[base - 1] : 0xffffffffu;
+    uint64_t starts = 0;
+    uint32_t vmax = 0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        const uint32_t p = j ? (uint32_t)r[j - 1] : prev;
+        if (r[j] != p) starts |= 1ULL << j;
+        vmax = r[j] > vmax ? r[j] : vmax;
+    }
+    uint32_t *s_first = L.idx;  // free until the updates start
+    s_first[t] = starts ? base + (uint32_t)__builtin_ctzll(starts) : 16384u;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {  // suffix minimum, in place
+        const uint32_t o = t + off < 256 ? s_first[t + off] : 16384u;
+        __syncthreads();
+        s_first[t] = min(s_first[t], o);
+        __syncthreads();
+    }
+    const uint32_t next_after = t + 1 < 256 ? s_first[t + 1] : 16384u;
+    uint32_t bytes = 0;
+    for (uint64_t m = starts; m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint64_t later = m & (m - 1);
+        const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
+        const uint32_t len = end - (base + j), v = r[j];
+        bytes += v == 0 ? (len > 64 ? 2u : 1u) : (len + 3) / 4;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        bytes += __shfl_down(bytes, off, 64);
+        vmax = max(vmax, (uint32_t)__shfl_down(vmax, off, 64));
+    }
+    if ((t & 63) == 0) {
+        L.part[t >> 6] = bytes;
+        L.part[4 + (t >> 6)] = vmax;
+    }
+    __syncthreads();
+    const uint32_t total = L.part[0] + L.part[1] + L.part[2] + L.part[3];
+    const uint32_t mx = max(max(L.part[4], L.part[5]), max(L.part[6], L.part[7]));
+    __syncthreads();  // part[] reuse
+    return mx > 32u || 16u + (uint64_t)total > max_bytes;
+}
+
 template <int ELEN>
 __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems, uint64_t max_bytes) {
     if (__hip_atomic_load(it.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // promoted: uniform
+    // (a SET string may already exceed the limit and stay sparse through updates that do not grow
+    // it: the length argument holds only for strings that start within the limit)
+    const uint64_t len0 = 16u + (it.state[1] ? it.state[2] : 2u);
+    if (must_promote(L, it.final_regs, len0 <= max_bytes ? max_bytes : ~0ULL)) {  // uniform
+        if (threadIdx.x == 0) it.state[0] = 1u;
+        return;
+    }
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     // load: opcode list -> run starts (thread t takes a contiguous slice of the list)
     const uint32_t nent = min(it.state[1], (uint32_t)kHllRegs);

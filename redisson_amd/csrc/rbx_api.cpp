@@ -1694,7 +1694,7 @@ static int replay_merge(rbx_ctx *c, const std::vector<HllState *> &hl, hipStream
     for (HllState *h : hl)
         if (h && !h->dense && !seen.count(h)) {
             seen[h] = 1;
-            items.push_back(HllReplay{h->d_sp_ops, h->d_promoted, h->d_regs, 0, 0});
+            items.push_back(HllReplay{h->d_sp_ops, h->d_promoted, h->d_regs, 0, 0, h->d_regs});
         }
     return replay_sparse(c, items, KeysDev{}, 0, st);
 }
@@ -1745,7 +1745,8 @@ static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64
             std::vector<HllReplay> items;  // the round's HLLs are distinct
             for (uint32_t s = s0; s < s1; ++s)
                 if (!hl[s]->dense && h_seg[s + 1] > h_seg[s])
-                    items.push_back(HllReplay{hl[s]->d_sp_ops, hl[s]->d_promoted, nullptr, h_seg[s], h_seg[s + 1]});
+                    items.push_back(HllReplay{hl[s]->d_sp_ops, hl[s]->d_promoted, nullptr, h_seg[s], h_seg[s + 1],
+                                              hl[s]->d_regs});
             RBX_TRY(replay_sparse(c, items, dk, fl, st));
         }
         s0 = s1;

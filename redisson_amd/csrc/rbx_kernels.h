@@ -230,6 +230,7 @@ struct HllReplay {
                           // createHLLObject string, one XZERO), [2] opcode bytes (after the header)
     const uint8_t *regs;  // merge mode (PFMERGE write-back): the max registers, ascending; else null
     uint64_t begin, end;  // PFADD mode: the command's elements, in order
+    const uint8_t *final_regs;  // the registers after the update (PFADD: the key's, merged already)
 };
 // one block per item; items whose HLL is already promoted return at once
 void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,

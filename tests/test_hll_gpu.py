@@ -428,3 +428,52 @@ def test_sparse_promotion_is_checked_per_command(client, fresh):
     ops = O.hll_sparse_pack(regs)
     assert 16 + len(ops) <= 3000  # what an export-time check would have kept sparse
     h.delete()
+
+
+def _count_elements(indexes, count, rng):
+    """One 16-byte element per register index whose MurmurHash64A gives that index and hllPatLen
+    `count` (bits 14 .. 14+count-2 of the hash clear, bit 14+count-1 set)."""
+    want = set(int(i) for i in indexes)
+    found = {}
+    sh = np.uint64(14)
+    while len(found) < len(want):
+        cand = rng.integers(0, 256, size=(1 << 20, 16), dtype=np.uint8)
+        h = O.murmur_batch(*O.fixed_arena(cand))
+        idx = (h & np.uint64(16383)).astype(np.int64)
+        low = (h >> sh) & np.uint64((1 << count) - 1)
+        ok = low == np.uint64(1 << (count - 1))
+        for j in np.nonzero(ok)[0]:
+            i = int(idx[j])
+            if i in want and i not in found:
+                found[i] = bytes(cand[j])
+    return [found[i] for i in sorted(want)]
+
+
+def test_sparse_set_string_beyond_limit(client, fresh):
+    """A SET sparse string longer than hll-sparse-max-bytes stays sparse through updates that do
+    not grow it (VAL of length 1 raised in place), and promotes at the first one that grows it."""
+    rng = np.random.default_rng(66)
+    ops = bytearray()
+    for _ in range(3000):  # registers 0, 2, .., 5998 = 1: 6000 opcode bytes
+        ops += bytes([0x80, 0x00])
+    rest = 16384 - 6000
+    ops += bytes([0x40 | ((rest - 1) >> 8), (rest - 1) & 0xFF])
+    s0 = _header(1, bytes(7) + b"\x80") + bytes(ops)
+    h = client.getHyperLogLog(fresh)
+    h.importString(s0)
+    ref = O.RedisHll.from_string(s0)
+    raise2 = _count_elements(range(0, 40, 2), 2, rng)  # VAL(1,1) -> VAL(2,1): no growth
+    assert h.addAll(Arena(raise2))
+    ref.pfadd(*O.arena(raise2))
+    s = h.exportString()
+    assert s[4] == 1 and len(s) == len(s0) and s == ref.string(s[8:16])
+    grow = _count_elements([1], 1, rng)  # ZERO(1) between two VALs -> VAL: no growth either
+    h.addAll(Arena(grow))
+    ref.pfadd(*O.arena(grow))
+    assert h.exportString() == ref.string(h.exportString()[8:16])
+    far = _count_elements([9000], 1, rng)  # splits the XZERO: grows past the limit -> dense
+    h.addAll(Arena(far))
+    ref.pfadd(*O.arena(far))
+    s = h.exportString()
+    assert s[4] == 0 and s == ref.string(s[8:16])
+    h.delete()
