@@ -220,6 +220,39 @@ def test_hll_pack_unpack_registers(client, fresh):
         L.lib().rbx_hll_close(h)
 
 
+def test_hll_unpack_max_keeps_sparse_strings(client, fresh):
+    """The exchange step's register merge into sparse keys follows pfmergeCommand's write-back
+    (hllSparseSet per register, ascending), so the stored strings equal the Redis restatement;
+    a merge that outgrows hll-sparse-max-bytes promotes."""
+    import torch
+
+    rng = np.random.default_rng(26)
+    names = [f"{fresh}-{i}" for i in range(3)]
+    refs = []
+    for nm in names:
+        m = rng.integers(0, 256, size=(200, 16), dtype=np.uint8)
+        client.getHyperLogLog(nm).addAll(Arena.fixed(m))
+        r = O.RedisHll()
+        r.pfadd(*O.fixed_arena(m))
+        refs.append(r)
+    hs, arr = _open_hlls(client, names)
+    other = np.zeros((3, 16384), np.uint8)
+    for i, n in enumerate((50, 300, 3000)):  # the third grows past the limit
+        pos = rng.choice(16384, size=n, replace=False)
+        other[i, pos] = rng.integers(1, 6, size=n)
+    buf = torch.from_numpy(other.reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    _check(L.lib().rbx_hll_unpack_max_registers(client.ctx, arr, 3, buf.data_ptr(), None))
+    L.lib().rbx_synchronize(client.ctx)
+    for i, nm in enumerate(names):
+        refs[i].merge_from(np.maximum(refs[i].regs, other[i]), use_dense=False)
+        s = client.getHyperLogLog(nm).exportString()
+        assert s == refs[i].string(s[8:16]), i
+    assert refs[2].dense.value and not refs[0].dense.value
+    for h in hs:
+        L.lib().rbx_hll_close(h)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
