@@ -220,10 +220,13 @@ __device__ __forceinline__ uint32_t value(uint32_t op) { return ((op >> 2) & 31u
 __device__ __forceinline__ uint32_t mkval(uint32_t v, uint32_t l) { return 0x80u | ((v - 1u) << 2) | (l - 1u); }
 __device__ __forceinline__ uint32_t mkzero(uint32_t l) { return l > 64u ? (0x4000u | (l - 1u)) : l - 1u; }
 
+// meta[r] for an opcode starting at register r is its Redis byte for ZERO and VAL, and 0x40 for
+// an XZERO, whose length is the distance to the next start (16 KiB of LDS, not 32: 21 KiB per
+// block, seven blocks per CU instead of four)
 struct Lds {
     unsigned long long bits[256];  // bit r: register r starts an opcode
     unsigned long long sum[4];     // bit w: bits[w] != 0
-    uint16_t meta[kHllRegs];       // the opcode starting at register r
+    uint8_t meta[kHllRegs];
     uint32_t idx[256];
     uint32_t cnt[256];
     unsigned long long mask[4];    // per wave: elements that raise their register
@@ -242,10 +245,31 @@ __device__ __forceinline__ uint32_t pred(const Lds &L, uint32_t r) {  // the sta
     return (w2 << 6) + 63u - (uint32_t)__builtin_clzll(L.bits[w2]);
 }
 
+__device__ __forceinline__ uint32_t succ(const Lds &L, uint32_t r) {  // the next start after r, or 16384
+    const uint32_t w = r >> 6, b = r & 63u;
+    const unsigned long long m = b == 63u ? 0ULL : L.bits[w] & (~0ULL << (b + 1u));
+    if (m) return (w << 6) + (uint32_t)__builtin_ctzll(m);
+    uint32_t sw = w >> 6;
+    unsigned long long mm = (w & 63u) == 63u ? 0ULL : L.sum[sw] & (~0ULL << ((w & 63u) + 1u));
+    while (!mm) {
+        if (++sw == 4u) return (uint32_t)kHllRegs;
+        mm = L.sum[sw];
+    }
+    const uint32_t w2 = (sw << 6) + (uint32_t)__builtin_ctzll(mm);
+    return (w2 << 6) + (uint32_t)__builtin_ctzll(L.bits[w2]);
+}
+
+__device__ __forceinline__ uint32_t opat(const Lds &L, uint32_t r) {  // the u16 opcode starting at r
+    const uint32_t b = L.meta[r];
+    return b == 0x40u ? 0x4000u | (succ(L, r) - r - 1u) : b;
+}
+
+__device__ __forceinline__ void put(Lds &L, uint32_t r, uint32_t op) { L.meta[r] = (uint8_t)(op >= 0x100u ? 0x40u : op); }
+
 __device__ __forceinline__ void set_start(Lds &L, uint32_t r, uint32_t op) {
     L.bits[r >> 6] |= 1ULL << (r & 63u);
     L.sum[r >> 12] |= 1ULL << ((r >> 6) & 63u);
-    L.meta[r] = (uint16_t)op;
+    put(L, r, op);
 }
 
 __device__ __forceinline__ void clear_start(Lds &L, uint32_t r) {
@@ -255,53 +279,46 @@ __device__ __forceinline__ void clear_start(Lds &L, uint32_t r) {
 }
 
 __device__ __forceinline__ uint32_t value_at(const Lds &L, uint32_t r) {
-    const uint32_t op = L.meta[pred(L, r)];
+    const uint32_t op = L.meta[pred(L, r)];  // (an XZERO's marker byte is not a VAL either)
     return is_val(op) ? value(op) : 0u;
 }
 
 // hllSparseSet on the LDS image (lane 0 only): 0 = no change, 1 = updated, 2 = promote
 __device__ uint32_t set(Lds &L, uint32_t index, uint32_t count, uint64_t max_bytes) {
     if (count > 32u) return 2u;  // HLL_SPARSE_VAL_MAX_VALUE
-    const uint32_t first = pred(L, index), op = L.meta[first], span = len(op), last = first + span - 1u;
+    const uint32_t first = pred(L, index), op = opat(L, first), span = len(op), last = first + span - 1u;
     if (is_val(op)) {
         if (value(op) >= count) return 0u;  // case A
         if (span == 1u) {                   // case B
-            L.meta[first] = (uint16_t)mkval(count, 1u);
+            put(L, first, mkval(count, 1u));
             goto updated;
         }
     } else if (!is_xzero(op) && span == 1u) {  // case C
-        L.meta[first] = (uint16_t)mkval(count, 1u);
+        put(L, first, mkval(count, 1u));
         goto updated;
     }
-    {  // case D: split into <= 3 opcodes
-        uint32_t q[3], qs[3], nq = 0, seq = 0;
-        const bool zero = !is_val(op);
+    {  // case D: split into <= 3 opcodes: [head at first] VAL(count, 1) at index [tail at index + 1]
+        const bool zero = !is_val(op), head = index != first, tail = index != last;
         const uint32_t cur = zero ? 0u : value(op);
-        if (index != first) {
-            q[nq] = zero ? mkzero(index - first) : mkval(cur, index - first);
-            qs[nq++] = first;
-        }
-        q[nq] = mkval(count, 1u);
-        qs[nq++] = index;
-        if (index != last) {
-            q[nq] = zero ? mkzero(last - index) : mkval(cur, last - index);
-            qs[nq++] = index + 1u;
-        }
-        for (uint32_t i = 0; i < nq; ++i) seq += bytes(q[i]);
+        const uint32_t qa = head ? (zero ? mkzero(index - first) : mkval(cur, index - first)) : 0u;
+        const uint32_t qc = tail ? (zero ? mkzero(last - index) : mkval(cur, last - index)) : 0u;
+        const uint32_t seq = 1u + (head ? bytes(qa) : 0u) + (tail ? bytes(qc) : 0u);
         const int delta = (int)seq - (int)bytes(op);
         if (delta > 0 && 16u + (uint64_t)L.nbytes + (uint64_t)delta > max_bytes) return 2u;
-        for (uint32_t i = 0; i < nq; ++i) set_start(L, qs[i], q[i]);
+        if (head) set_start(L, first, qa);
+        set_start(L, index, mkval(count, 1u));
+        if (tail) set_start(L, index + 1u, qc);
         L.nbytes = (uint32_t)((int)L.nbytes + delta);
     }
 updated:
     {  // merge adjacent VALs of one value, scanning up to 5 opcodes from the previous one
         uint32_t p = first ? pred(L, first - 1u) : 0u;
         for (int scan = 5; p < (uint32_t)kHllRegs && scan-- > 0;) {
-            const uint32_t o = L.meta[p], nx = p + len(o);
+            const uint32_t o = opat(L, p), nx = p + len(o);
             if (is_val(o) && nx < (uint32_t)kHllRegs) {
                 const uint32_t o2 = L.meta[nx];
                 if (is_val(o2) && value(o2) == value(o) && len(o) + len(o2) <= 4u) {
-                    L.meta[p] = (uint16_t)mkval(value(o), len(o) + len(o2));
+                    put(L, p, mkval(value(o), len(o) + len(o2)));
                     clear_start(L, nx);
                     L.nbytes -= 1u;
                     continue;  // the merged opcode may merge again
@@ -341,23 +358,21 @@ __device__ __forceinline__ uint32_t block_scan(Lds &L, uint32_t v, uint32_t &exc
 // registers [64t, 64t + 64); a run is charged by the thread holding its first register, which
 // finds the run's end through a suffix minimum of the threads' first run starts.
 __device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes) {
-    typedef unsigned char u8x16v __attribute__((ext_vector_type(16)));
     const uint32_t t = threadIdx.x, base = t * 64;
-    uint8_t r[64];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const u8x16v v = ((const u8x16v *)(regs + base))[q];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) r[q * 16 + j] = v[j];
-    }
-    const uint32_t prev = t ? regs[base - 1] : 0xffffffffu;
+    const uint32_t *w = (const uint32_t *)(regs + base);  // the thread's 64 registers, a word at a time
+    uint32_t p = t ? regs[base - 1] : 0xffffffffu;
     uint64_t starts = 0;
     uint32_t vmax = 0;
+#pragma unroll 1
+    for (uint32_t q = 0; q < 16; ++q) {
+        const uint32_t wq = w[q];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        const uint32_t p = j ? (uint32_t)r[j - 1] : prev;
-        if (r[j] != p) starts |= 1ULL << j;
-        vmax = r[j] > vmax ? r[j] : vmax;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t r = (wq >> (8 * b)) & 0xffu;
+            if (r != p) starts |= 1ULL << (4 * q + b);
+            vmax = r > vmax ? r : vmax;
+            p = r;
+        }
     }
     uint32_t *s_first = L.idx;  // free until the updates start
     s_first[t] = starts ? base + (uint32_t)__builtin_ctzll(starts) : 16384u;
@@ -374,7 +389,7 @@ __device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes
         const uint32_t j = (uint32_t)__builtin_ctzll(m);
         const uint64_t later = m & (m - 1);
         const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
-        const uint32_t len = end - (base + j), v = r[j];
+        const uint32_t len = end - (base + j), v = regs[base + j];  // (cached: read above)
         bytes += v == 0 ? (len > 64 ? 2u : 1u) : (len + 3) / 4;
     }
 #pragma unroll
@@ -421,13 +436,13 @@ __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems
         const uint32_t op = it.ops[e];
         if (start < (uint32_t)kHllRegs) {
             atomicOr(&L.bits[start >> 6], 1ULL << (start & 63u));
-            L.meta[start] = (uint16_t)op;
+            sp::put(L, start, op);
         }
         start += sp::len(op);
     }
     if (nent == 0 && t == 0) {  // createHLLObject: XZERO over the 16384 registers
         L.bits[0] = 1ULL;
-        L.meta[0] = 0x7fffu;
+        L.meta[0] = 0x40u;  // XZERO to the end
     }
     __syncthreads();
     {
@@ -483,17 +498,17 @@ __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems
     const unsigned long long w = L.bits[t];
     uint32_t pos;
     const uint32_t total = sp::block_scan(L, (uint32_t)__builtin_popcountll(w), pos);
-    for (unsigned long long m = w; m; m &= m - 1) it.ops[pos++] = L.meta[t * 64u + (uint32_t)__builtin_ctzll(m)];
+    for (unsigned long long m = w; m; m &= m - 1) it.ops[pos++] = (uint16_t)sp::opat(L, t * 64u + (uint32_t)__builtin_ctzll(m));
     if (t == 0) {
         it.state[1] = total;
         it.state[2] = L.nbytes;
     }
 }
 
-// a grid of <= 2048 blocks walks the items: a steady PFADD stream into keys that have been
+// a grid of <= 1792 blocks walks the items: a steady PFADD stream into keys that have been
 // promoted (the host learns promotions lazily) costs one state load per key, not one block
 template <int ELEN>
-__global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const HllReplay *__restrict__ items,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_hll_sparse_replay(KeysDev elems, const HllReplay *__restrict__ items,
                                                            uint32_t n, uint64_t max_bytes) {
     __shared__ sp::Lds L;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(256) void k_hll_sparse_replay(KeysDev elems, const 
 void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,
                               uint64_t max_bytes, hipStream_t st) {
     if (!n) return;
-    const dim3 grid(std::min<uint32_t>(n, 2048));
+    const dim3 grid(std::min<uint32_t>(n, 7 * 256));  // seven 21 KiB blocks per CU, all resident
     switch (elen_fast) {
     case 16: hipLaunchKernelGGL(k_hll_sparse_replay<16>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
     case 32: hipLaunchKernelGGL(k_hll_sparse_replay<32>, grid, dim3(256), 0, st, elems, items, n, max_bytes); break;
