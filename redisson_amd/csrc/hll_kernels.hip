@@ -234,59 +234,82 @@ struct Lds {
     uint32_t nbytes, state, changed;
 };
 
-__device__ __forceinline__ uint32_t pred(const Lds &L, uint32_t r) {  // the start covering r
+// The bitmap summary as lane 0 holds it while it applies a batch (registers, not LDS: the
+// replay is a chain of dependent single-lane accesses), with its running string length.
+struct Hot {
+    unsigned long long s0, s1, s2, s3;
+    uint32_t nbytes;
+    __device__ __forceinline__ unsigned long long operator[](uint32_t i) const {
+        return i == 0u ? s0 : (i == 1u ? s1 : (i == 2u ? s2 : s3));
+    }
+    __device__ __forceinline__ void set(uint32_t i, unsigned long long v) {
+        if (i == 0u) s0 = v;
+        else if (i == 1u) s1 = v;
+        else if (i == 2u) s2 = v;
+        else s3 = v;
+    }
+};
+struct LdsSum {
+    const unsigned long long *p;
+    __device__ __forceinline__ unsigned long long operator[](uint32_t i) const { return p[i]; }
+};
+
+template <class S>
+__device__ __forceinline__ uint32_t pred(const Lds &L, const S &sum, uint32_t r) {  // the start covering r
     const uint32_t w = r >> 6;
     const unsigned long long m = L.bits[w] & (~0ULL >> (63u - (r & 63u)));
     if (m) return (w << 6) + 63u - (uint32_t)__builtin_clzll(m);
     int sw = (int)(w >> 6);
-    unsigned long long mm = L.sum[sw] & ((1ULL << (w & 63u)) - 1ULL);
-    while (!mm) mm = L.sum[--sw];  // register 0 always starts an opcode
+    unsigned long long mm = sum[(uint32_t)sw] & ((1ULL << (w & 63u)) - 1ULL);
+    while (!mm) mm = sum[(uint32_t)(--sw)];  // register 0 always starts an opcode
     const uint32_t w2 = ((uint32_t)sw << 6) + 63u - (uint32_t)__builtin_clzll(mm);
     return (w2 << 6) + 63u - (uint32_t)__builtin_clzll(L.bits[w2]);
 }
 
-__device__ __forceinline__ uint32_t succ(const Lds &L, uint32_t r) {  // the next start after r, or 16384
+template <class S>
+__device__ __forceinline__ uint32_t succ(const Lds &L, const S &sum, uint32_t r) {  // next start after r, or 16384
     const uint32_t w = r >> 6, b = r & 63u;
     const unsigned long long m = b == 63u ? 0ULL : L.bits[w] & (~0ULL << (b + 1u));
     if (m) return (w << 6) + (uint32_t)__builtin_ctzll(m);
     uint32_t sw = w >> 6;
-    unsigned long long mm = (w & 63u) == 63u ? 0ULL : L.sum[sw] & (~0ULL << ((w & 63u) + 1u));
+    unsigned long long mm = (w & 63u) == 63u ? 0ULL : sum[sw] & (~0ULL << ((w & 63u) + 1u));
     while (!mm) {
         if (++sw == 4u) return (uint32_t)kHllRegs;
-        mm = L.sum[sw];
+        mm = sum[sw];
     }
     const uint32_t w2 = (sw << 6) + (uint32_t)__builtin_ctzll(mm);
     return (w2 << 6) + (uint32_t)__builtin_ctzll(L.bits[w2]);
 }
 
-__device__ __forceinline__ uint32_t opat(const Lds &L, uint32_t r) {  // the u16 opcode starting at r
+template <class S>
+__device__ __forceinline__ uint32_t opat(const Lds &L, const S &sum, uint32_t r) {  // the u16 opcode at r
     const uint32_t b = L.meta[r];
-    return b == 0x40u ? 0x4000u | (succ(L, r) - r - 1u) : b;
+    return b == 0x40u ? 0x4000u | (succ(L, sum, r) - r - 1u) : b;
 }
 
 __device__ __forceinline__ void put(Lds &L, uint32_t r, uint32_t op) { L.meta[r] = (uint8_t)(op >= 0x100u ? 0x40u : op); }
 
-__device__ __forceinline__ void set_start(Lds &L, uint32_t r, uint32_t op) {
+__device__ __forceinline__ void set_start(Lds &L, Hot &H, uint32_t r, uint32_t op) {
     L.bits[r >> 6] |= 1ULL << (r & 63u);
-    L.sum[r >> 12] |= 1ULL << ((r >> 6) & 63u);
+    H.set(r >> 12, H[r >> 12] | (1ULL << ((r >> 6) & 63u)));
     put(L, r, op);
 }
 
-__device__ __forceinline__ void clear_start(Lds &L, uint32_t r) {
+__device__ __forceinline__ void clear_start(Lds &L, Hot &H, uint32_t r) {
     const unsigned long long b = L.bits[r >> 6] & ~(1ULL << (r & 63u));
     L.bits[r >> 6] = b;
-    if (!b) L.sum[r >> 12] &= ~(1ULL << ((r >> 6) & 63u));
+    if (!b) H.set(r >> 12, H[r >> 12] & ~(1ULL << ((r >> 6) & 63u)));
 }
 
 __device__ __forceinline__ uint32_t value_at(const Lds &L, uint32_t r) {
-    const uint32_t op = L.meta[pred(L, r)];  // (an XZERO's marker byte is not a VAL either)
+    const uint32_t op = L.meta[pred(L, LdsSum{L.sum}, r)];  // (an XZERO's marker byte is not a VAL either)
     return is_val(op) ? value(op) : 0u;
 }
 
 // hllSparseSet on the LDS image (lane 0 only): 0 = no change, 1 = updated, 2 = promote
-__device__ uint32_t set(Lds &L, uint32_t index, uint32_t count, uint64_t max_bytes) {
+__device__ uint32_t set(Lds &L, Hot &H, uint32_t index, uint32_t count, uint64_t max_bytes) {
     if (count > 32u) return 2u;  // HLL_SPARSE_VAL_MAX_VALUE
-    const uint32_t first = pred(L, index), op = opat(L, first), span = len(op), last = first + span - 1u;
+    const uint32_t first = pred(L, H, index), op = opat(L, H, first), span = len(op), last = first + span - 1u;
     if (is_val(op)) {
         if (value(op) >= count) return 0u;  // case A
         if (span == 1u) {                   // case B
@@ -304,23 +327,23 @@ __device__ uint32_t set(Lds &L, uint32_t index, uint32_t count, uint64_t max_byt
         const uint32_t qc = tail ? (zero ? mkzero(last - index) : mkval(cur, last - index)) : 0u;
         const uint32_t seq = 1u + (head ? bytes(qa) : 0u) + (tail ? bytes(qc) : 0u);
         const int delta = (int)seq - (int)bytes(op);
-        if (delta > 0 && 16u + (uint64_t)L.nbytes + (uint64_t)delta > max_bytes) return 2u;
-        if (head) set_start(L, first, qa);
-        set_start(L, index, mkval(count, 1u));
-        if (tail) set_start(L, index + 1u, qc);
-        L.nbytes = (uint32_t)((int)L.nbytes + delta);
+        if (delta > 0 && 16u + (uint64_t)H.nbytes + (uint64_t)delta > max_bytes) return 2u;
+        if (head) set_start(L, H, first, qa);
+        set_start(L, H, index, mkval(count, 1u));
+        if (tail) set_start(L, H, index + 1u, qc);
+        H.nbytes = (uint32_t)((int)H.nbytes + delta);
     }
 updated:
     {  // merge adjacent VALs of one value, scanning up to 5 opcodes from the previous one
-        uint32_t p = first ? pred(L, first - 1u) : 0u;
+        uint32_t p = first ? pred(L, H, first - 1u) : 0u;
         for (int scan = 5; p < (uint32_t)kHllRegs && scan-- > 0;) {
-            const uint32_t o = opat(L, p), nx = p + len(o);
+            const uint32_t o = opat(L, H, p), nx = p + len(o);
             if (is_val(o) && nx < (uint32_t)kHllRegs) {
                 const uint32_t o2 = L.meta[nx];
                 if (is_val(o2) && value(o2) == value(o) && len(o) + len(o2) <= 4u) {
                     put(L, p, mkval(value(o), len(o) + len(o2)));
-                    clear_start(L, nx);
-                    L.nbytes -= 1u;
+                    clear_start(L, H, nx);
+                    H.nbytes -= 1u;
                     continue;  // the merged opcode may merge again
                 }
             }
@@ -474,17 +497,26 @@ __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems
         if (lane == 0) L.mask[wave] = m;
         __syncthreads();
         if (t == 0) {
-            for (uint32_t w = 0; w < 4u && !L.state; ++w) {
+            sp::Hot H{L.sum[0], L.sum[1], L.sum[2], L.sum[3], L.nbytes};
+            uint32_t state = 0, changed = 0;
+            for (uint32_t w = 0; w < 4u && !state; ++w) {
                 for (unsigned long long mm = L.mask[w]; mm; mm &= mm - 1) {
                     const uint32_t i = w * 64u + (uint32_t)__builtin_ctzll(mm);
-                    const uint32_t r = sp::set(L, L.idx[i], L.cnt[i], max_bytes);
+                    const uint32_t r = sp::set(L, H, L.idx[i], L.cnt[i], max_bytes);
                     if (r == 2u) {
-                        L.state = 1;
+                        state = 1;
                         break;
                     }
-                    L.changed |= r;
+                    changed |= r;
                 }
             }
+            L.sum[0] = H.s0;
+            L.sum[1] = H.s1;
+            L.sum[2] = H.s2;
+            L.sum[3] = H.s3;
+            L.nbytes = H.nbytes;
+            L.state = state;
+            L.changed |= changed;
         }
         __syncthreads();
         if (L.state) break;  // uniform
@@ -498,7 +530,8 @@ __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems
     const unsigned long long w = L.bits[t];
     uint32_t pos;
     const uint32_t total = sp::block_scan(L, (uint32_t)__builtin_popcountll(w), pos);
-    for (unsigned long long m = w; m; m &= m - 1) it.ops[pos++] = (uint16_t)sp::opat(L, t * 64u + (uint32_t)__builtin_ctzll(m));
+    for (unsigned long long m = w; m; m &= m - 1)
+        it.ops[pos++] = (uint16_t)sp::opat(L, sp::LdsSum{L.sum}, t * 64u + (uint32_t)__builtin_ctzll(m));
     if (t == 0) {
         it.state[1] = total;
         it.state[2] = L.nbytes;
