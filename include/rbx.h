@@ -397,8 +397,11 @@ int rbx_node_bloom_add_multi(rbx_node *node, const rbx_name *names, uint32_t nse
 /* PFADD commands routed per name (commands on one name keep their order) */
 int rbx_node_hll_add_multi(rbx_node *node, const rbx_name *names, uint32_t nseg, const uint64_t *seg_offsets,
                            const rbx_keys *elements, uint8_t *out_changed);
-/* PFCOUNT / PFMERGE over names that may live on different GPUs: the registers of the other GPUs'
- * HLLs are staged through the host (their Redis strings, encoding kept) */
+/* PFCOUNT / PFMERGE over names that may live on different GPUs: every HLL held by another GPU is
+ * peer-copied device to device (rbx_hll_copy_to: registers, encoding, cached cardinality and the
+ * sparse string, over xGMI on a multi-GPU node) into a temporary key on the GPU of the first name
+ * (PFCOUNT) or of the destination (PFMERGE), which is deleted after the call -- no host staging.
+ * M/RedissonHyperLogLog.java:89-102 (countWith / mergeWith). */
 int rbx_node_hll_count(rbx_node *node, const rbx_name *names, uint32_t n, uint64_t *out);
 int rbx_node_hll_merge(rbx_node *node, rbx_name dest, const rbx_name *srcs, uint32_t nsrc);
 

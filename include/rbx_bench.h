@@ -59,6 +59,8 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44
  *   "contains_qgrid"        slot kernel grid, 256..8192 (default 2048)
  *   "stream_contains_slots" ordered-stream contains: 0 staged kernel (default), 1 slot kernel
+ *   "stream_table8"         ordered stream's first-setter table: 1 (default) 8-byte entries claimed
+ *                           by one CAS and committed by a table walk, 0 the 16-byte epoch-tagged table
  *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
  *                           resident blocks (default 33000: four per CU; 0: registers decide)
  *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,
@@ -68,6 +70,10 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather)
  *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048) */
 int rbx_tune(const char *key, int value);
+/* Test hook (fault injection): the next n Bloom adds that the node runs on GPU `gpu` (single or
+ * multi-tenant, replica or home) fail with RBX_E_DEVICE before they touch the device; n = 0 clears.
+ * Exercises the replicated-add failure semantics of rbx_node_bloom_replicate. */
+int rbx_node_test_fail_adds(rbx_node *node, int gpu, int n);
 #ifdef __cplusplus
 }
 #endif

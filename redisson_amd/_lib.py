@@ -167,6 +167,7 @@ SIGNATURES = {
     "rbx_node_hll_merge": (C.c_int, [vp, RbxName, C.POINTER(RbxName), C.c_uint32]),
     "rbx_node_bloom_replicate": (C.c_int, [vp, RbxName, C.c_int]),
     "rbx_node_bloom_is_replicated": (C.c_int, [vp, RbxName, C.POINTER(C.c_int)]),
+    "rbx_node_test_fail_adds": (C.c_int, [vp, C.c_int, C.c_int]),
     # replicas
     "rbx_bloom_digest": (C.c_int, [vp, C.c_char_p, u64p]),
     "rbx_bloom_digest_n": (C.c_int, [vp, RbxName, u64p]),

@@ -576,6 +576,41 @@ __device__ __forceinline__ uint32_t ht_find(const HTEntry *__restrict__ T, uint3
     return 0xffffffffu;
 }
 
+// 8-byte stream first-setter entries (r04; see k_stream_probe8)
+__device__ __forceinline__ uint64_t t8_slot(uint64_t key, uint32_t lg) {
+    return ((key + 1) * 0x9E3779B97F4A7C15ULL) >> (64 - lg);
+}
+
+__device__ __forceinline__ void t8_insert(unsigned long long *__restrict__ T, uint32_t lg, uint32_t pb, uint64_t key,
+                                          uint32_t pos) {
+    const uint64_t mask = (1ULL << lg) - 1;
+    const unsigned long long mine = ((unsigned long long)key << pb) | pos;
+    uint64_t slot = t8_slot(key, lg);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long old = atomicCAS(&T[slot], ~0ULL, mine);
+        if (old == ~0ULL) return;
+        if ((old >> pb) == key) {
+            if (old > mine) atomicMin(&T[slot], mine);
+            return;
+        }
+        slot = (slot + 1) & mask;
+    }
+}
+
+// the first setter's chunk position of key, ~0u when no add of the chunk meets it at 0
+__device__ __forceinline__ uint32_t t8_find(const unsigned long long *__restrict__ T, uint32_t lg, uint32_t pb,
+                                            uint64_t key) {
+    const uint64_t mask = (1ULL << lg) - 1;
+    uint64_t slot = t8_slot(key, lg);
+    for (uint64_t probes = 0; probes <= mask; ++probes) {
+        const unsigned long long e = T[slot];
+        if (e == ~0ULL) return 0xffffffffu;
+        if ((e >> pb) == key) return (uint32_t)(e & ((1ULL << pb) - 1));
+        slot = (slot + 1) & mask;
+    }
+    return 0xffffffffu;
+}
+
 // ---- ordered mixed stream (C5): key i is a single-key contains (op 0) or add (op 1) on
 // filters[kf[i]], executed in key order.  Per chunk: compact the adds' positions, probe the adds
 // (first-setter table of add positions per initially-zero bit, plus a prefilter bitset of the
@@ -678,8 +713,11 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
                                                          uint32_t epoch, const uint32_t *__restrict__ prefilter,
                                                          uint32_t pshift,
                                                          uint8_t *__restrict__ out,
-                                                         unsigned long long *__restrict__ counts) {
+                                                         unsigned long long *__restrict__ counts,
+                                                         const unsigned long long *__restrict__ T8, uint32_t bb,
+                                                         uint32_t pb, uint32_t kmax, const uint32_t *__restrict__ nadds) {
     uint64_t present = 0;
+    const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
         const uint64_t i = base + t;
@@ -707,9 +745,10 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
             for (int u = 0; u < KMAX; ++u) {
                 if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
                     // set by an earlier add of this chunk?  Only possible if the prefilter says so.
-                    const uint32_t pb = prefilter_bit(f.fid, idxs[u], pshift);
-                    if (!prefilter || ((prefilter[pb >> 5] >> (pb & 31)) & 1u)) {
-                        const uint32_t owner = ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
+                    const uint32_t pfb = prefilter_bit(f.fid, idxs[u], pshift);
+                    if (!prefilter || ((prefilter[pfb >> 5] >> (pfb & 31)) & 1u)) {
+                        const uint32_t owner = T8 ? t8_find(T8, lg8, pb, ((uint64_t)f.fid << bb) | idxs[u])
+                                                  : ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
                         all = owner < (uint32_t)t;
                     } else {
                         all = false;
@@ -737,8 +776,12 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                                                            uint32_t epoch, const uint32_t *__restrict__ prefilter,
                                                            uint32_t pshift,
                                                            uint8_t *__restrict__ out,
-                                                           unsigned long long *__restrict__ counts) {
+                                                           unsigned long long *__restrict__ counts,
+                                                           const unsigned long long *__restrict__ T8, uint32_t bb,
+                                                           uint32_t pb, uint32_t kmax,
+                                                           const uint32_t *__restrict__ nadds) {
     constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
+    const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
     struct alignas(16) QEnt {
         uint64_t h1, h2;
         uint32_t t, fi, idx0, pad;  // chunk-local command index, filter index, first bit
@@ -843,9 +886,10 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
             if (act[s]) {
                 bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
                 if (clear) {  // set by an earlier add of this chunk?  Only if the prefilter says so.
-                    const uint32_t pb = prefilter_bit(sfid[s], sidx[s], pshift);
-                    if (!prefilter || ((prefilter[pb >> 5] >> (pb & 31)) & 1u))
-                        clear = !(ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s]) < st[s]);
+                    const uint32_t pfb = prefilter_bit(sfid[s], sidx[s], pshift);
+                    if (!prefilter || ((prefilter[pfb >> 5] >> (pfb & 31)) & 1u))
+                        clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
+                                      : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
                 }
                 bool fin = clear;
                 if (!clear && ((++sjk[s]) & 0xffffu) >= (sjk[s] >> 16)) {
@@ -900,6 +944,101 @@ __global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t ba
         }
         if (out) out[i] = isnew;
         added += isnew;
+    }
+    if (counts) block_add_u64(added, counts + 1);
+}
+
+// ---- ordered stream, r04: 8-byte first-setter entries, committed by a table walk -------------
+// The r03 probe spent ~15 memory requests per add: per zero bit a tag load, a CAS and
+// an atomicMin on a 16-byte entry of a 2 GiB epoch-tagged table, plus the commit's re-hash, zmask
+// read and owner lookup per zero bit.  Here an entry is ONE word, (fid << bb | bit) << pb | position:
+// a zero bit is claimed by one CAS on an empty slot (a slot already holding the bit takes an
+// atomicMin -- same high bits, so the minimum is the first setter), the table is sized to the
+// chunk's adds (2^t8_log2 entries, e.g. 8M = 64 MiB for C5's 671K adds), and the commit is a
+// streaming walk over it: every entry is an owned bit (its minimum position is the first add that
+// meets it at 0), so the walk ORs the bit into its bitmap, flags its owner and empties the slot.
+// A final pass over the add list turns the flags into replies and the new-add count.
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t base, const uint32_t *__restrict__ adds,
+                                                       const uint32_t *__restrict__ nadds,
+                                                       const FilterDesc *__restrict__ filt,
+                                                       const uint32_t *__restrict__ kf, unsigned long long *__restrict__ T,
+                                                       uint32_t bb, uint32_t pb, uint32_t kmax,
+                                                       uint32_t *__restrict__ prefilter, uint32_t pshift) {
+    const uint32_t na = *nadds;
+    const uint32_t lg = t8_log2(na, kmax);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
+        const uint32_t t = adds[a];
+        const uint64_t i = base + t;
+        const FilterDesc f = filt[kf[i]];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint32_t maxidx = 0;
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+                t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
+                if (prefilter) {
+                    const uint32_t pb2 = prefilter_bit(f.fid, idxs[j], pshift);
+                    atomicOr(&prefilter[pb2 >> 5], 1u << (pb2 & 31));
+                }
+            }
+        }
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+// every entry: OR its bit into its bitmap, flag its owner, empty the slot (two entries per lane)
+__global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restrict__ T, const uint32_t *__restrict__ nadds,
+                                                     uint32_t kmax, uint32_t bb, uint32_t pb,
+                                                     uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag) {
+    const uint32_t lg = t8_log2(*nadds, kmax);
+    const uint64_t n2 = (1ULL << lg) / 2;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t pmask = (1ULL << pb) - 1, bmask = (1ULL << bb) - 1;
+    using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n2; q += stride) {
+        u64x2 e = ((const u64x2 *)T)[q];
+        if ((e.x & e.y) == ~0ULL) continue;  // both empty
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const unsigned long long v = h ? e.y : e.x;
+            if (v == ~0ULL) continue;
+            const uint64_t key = v >> pb;
+            const uint32_t bit = (uint32_t)(key & bmask);
+            atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
+            flag[v & pmask] = 1;
+        }
+        ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
+    }
+}
+
+// replies and the new-add count from the owner flags; the flags are cleared for the next chunk
+__global__ __launch_bounds__(256) void k_stream_final(uint64_t base, const uint32_t *__restrict__ adds,
+                                                      const uint32_t *__restrict__ nadds, uint8_t *__restrict__ flag,
+                                                      uint8_t *__restrict__ out, unsigned long long *__restrict__ counts) {
+    uint64_t added = 0;
+    const uint32_t na = *nadds;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
+        const uint32_t t = adds[a];
+        const uint8_t v = flag[t];
+        if (v) flag[t] = 0;
+        if (out) out[base + t] = v;
+        added += v;
     }
     if (counts) block_add_u64(added, counts + 1);
 }
@@ -1309,17 +1448,28 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned cgrid = (unsigned)((a.nchunk + 4095) / 4096);
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
-    hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
+    if (a.t8)
+        hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.kmax, a.prefilter, a.pshift);
+    else
+        hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                           a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
                            a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
-                           a.pshift, a.out, a.counts);
+                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.kmax, a.nadds);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
-                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts);
-    hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                       a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
+                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
+                           a.t8, a.bb, a.pb, a.kmax, a.nadds);
+    if (a.t8) {
+        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.kmax, a.bb, a.pb, a.fid_bm,
+                           a.flag);
+        hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);
+    } else {
+        hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                           a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
+    }
 }
 
 template <int KLEN>

@@ -134,6 +134,8 @@ struct HllState {  // a Redis HLL string, registers unpacked (1 byte each) on th
     // string to dense --, [1] opcodes in d_sp_ops (0 = the createHLLObject string), [2] its bytes
     uint32_t *d_promoted = nullptr;
     uint16_t *d_sp_ops = nullptr;  // the sparse string as Redis built it, one u16 per opcode
+    uint16_t *d_slot_ops = nullptr;  // the pool slot's opcode list (kHllSlotOps entries)
+    uint16_t *d_big_ops = nullptr;   // own allocation (16384 entries) for a SET string past the slot
     uint64_t card = 0;          // the header's 8 cached-cardinality bytes (LE); bit 63 = invalid
     bool dense = false;         // Redis encoding: created sparse, promoted to dense once (never back)
     struct ::rbx_ctx *owner = nullptr;
@@ -185,6 +187,11 @@ struct rbx_ctx {
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf pa_stamps;  // add_partition_diag & 64: region-pass phase times (rbx_bench_add_stamps)
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
+    DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
+    uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
+    DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
+    uint32_t filt_nfids = 0;     // distinct table ids of filt_table
+    uint64_t filt_maxbits = 0;   // the largest of their bitmaps, in bits
     // all-zero words standing in for a missing bitmap in multi-tenant contains (GETBIT on a
     // missing key reads 0; the key is not created), grown on demand, never written by a kernel
     DevBuf zero_bm;
@@ -260,16 +267,37 @@ struct ScratchOrder {
 static constexpr size_t kHllBytes = 16384;
 static constexpr size_t kHllPerChunk = 4096;  // 192 MiB per pool chunk
 static constexpr size_t kHllStateWords = 4;   // HllReplay::state, 16 bytes
-static constexpr size_t kHllOpsBytes = 16384 * 2;  // a sparse string has <= 16384 opcodes
+// Opcode list capacity per pooled HLL.  A sparse string's opcodes never outnumber its bytes, and
+// hllSparseSet promotes instead of growing a string past hll-sparse-max-bytes (3000), so a
+// PFADD-built string fits 3072 entries (6 KiB per HLL instead of 32 KiB); a SET string
+// longer than that (up to 16384 opcodes) moves to its own allocation (hll_ops_reserve), and
+// from then on it can only shrink or promote.
+static constexpr size_t kHllSlotOps = 3072;
+static constexpr size_t kHllOpsBytes = kHllSlotOps * 2;
+static constexpr size_t kHllMaxOps = 16384;
 
 rbx::HllState::~HllState() {
     if (d_regs && owner) {
         {
             std::lock_guard<std::recursive_mutex> g(owner->ks.mu);
-            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted, d_sp_ops});
+            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted, d_slot_ops});
+            if (d_big_ops && !owner->shut) (void)hipFree(d_big_ops);
         }
         ctx_release(owner);
     }
+}
+
+// room for `nops` opcodes in h's list (the caller then overwrites the list)
+static int hll_ops_reserve(HllState *h, uint64_t nops) {
+    if (nops <= kHllSlotOps || h->d_big_ops) {
+        if (nops > kHllMaxOps) return fail(RBX_E_WRONGTYPE, "a sparse HLL string holds at most 16384 opcodes");
+        if (h->d_big_ops) h->d_sp_ops = h->d_big_ops;
+        return RBX_OK;
+    }
+    if (nops > kHllMaxOps) return fail(RBX_E_WRONGTYPE, "a sparse HLL string holds at most 16384 opcodes");
+    HIP_TRY(hipMalloc(&h->d_big_ops, kHllMaxOps * 2));
+    h->d_sp_ops = h->d_big_ops;
+    return RBX_OK;
 }
 
 // A fresh zeroed HLL register block; the fill runs on `st` (see SlabPool).
@@ -288,7 +316,7 @@ static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out)
     auto h = std::make_shared<HllState>();
     h->d_regs = c->hll_free.back().regs;
     h->d_promoted = c->hll_free.back().state;
-    h->d_sp_ops = c->hll_free.back().ops;
+    h->d_sp_ops = h->d_slot_ops = c->hll_free.back().ops;
     c->hll_free.pop_back();
     h->owner = c;
     c->refs.fetch_add(1);
@@ -1415,6 +1443,19 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
         for (size_t s = 0; s < v.size(); ++s) pd[s] = ProbeDesc{v[s].bm, mod_compact(v[s].mp), v[s].k, v[s].fid};
         RBX_TRY(c->probe_table.reserve(pd.size() * sizeof(ProbeDesc)));
         HIP_TRY(hipMemcpyAsync(c->probe_table.p, pd.data(), pd.size() * sizeof(ProbeDesc), hipMemcpyHostToDevice, st));
+        // bitmap words per fid (the stream's table walk finds a bit's bitmap by its fid)
+        uint32_t nf = 0;
+        uint64_t maxbits = 1;
+        for (size_t s = 0; s < v.size(); ++s) {
+            nf = std::max(nf, v[s].fid + 1);
+            maxbits = std::max<uint64_t>(maxbits, v[s].mp.size);
+        }
+        std::vector<uint32_t *> fb(std::max<uint32_t>(nf, 1), nullptr);
+        for (size_t s = 0; s < v.size(); ++s) fb[v[s].fid] = v[s].bm;
+        RBX_TRY(c->fid_table.reserve(fb.size() * sizeof(uint32_t *)));
+        HIP_TRY(hipMemcpyAsync(c->fid_table.p, fb.data(), fb.size() * sizeof(uint32_t *), hipMemcpyHostToDevice, st));
+        c->filt_nfids = nf;
+        c->filt_maxbits = maxbits;
         c->filt_cache.swap(v);
         c->filt_generation = c->ks.generation;
     }
@@ -1478,6 +1519,9 @@ static uint64_t g_stream_chunk = 0;
 // contains reads before it looks a clear bit up in the first-setter table (default 23: 1 MiB);
 // 0 = the table alone (measured slower: 10.3 -> 10.8 ms per 1e8 C5 commands)
 static int g_stream_prefilter = 23;
+// rbx_tune("stream_table8"): 1 (default) the 8-byte first-setter table + walk commit (r04) when
+// (fid, bit) fits 41 bits, 0 the r03 16-byte epoch-tagged table
+static int g_stream_table8 = 1;
 int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
                          const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
                          unsigned long long *d_counts, void *stream) {
@@ -1502,10 +1546,39 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     const uint64_t kPrefilterWords = 1ULL << (pbits - 5);
     RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
     const int fl = fast_len(keys);
+    // r04: 8-byte first-setter entries when (fid, bit) leaves >= 23 bits for a chunk position
+    uint32_t bb = 1, fbits = 0;
+    while ((1ULL << bb) < c->filt_maxbits) ++bb;
+    while ((1ULL << fbits) < c->filt_nfids) ++fbits;
+    const bool t8 = g_stream_table8 && bb + fbits <= 41;
+    const uint32_t pb = 64 - bb - fbits;
+    if (t8) {
+        chunk = std::min<uint64_t>(chunk, std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, 1ULL << 30));
+        const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)k);
+        if (c->st_t8_entries < entries) {
+            c->st_t8_entries = 0;
+            RBX_TRY(c->st_t8.reserve(entries * 8));
+            HIP_TRY(hipMemsetAsync(c->st_t8.p, 0xff, entries * 8, st));
+            c->st_t8_entries = entries;
+        }
+        if (c->st_flag_bytes < chunk) {
+            c->st_flag_bytes = 0;
+            RBX_TRY(c->st_flag.reserve(chunk));
+            HIP_TRY(hipMemsetAsync(c->st_flag.p, 0, chunk, st));
+            c->st_flag_bytes = chunk;
+        }
+    }
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
-        RBX_TRY(ensure_table(c, nch * k, st));
+        if (!t8) RBX_TRY(ensure_table(c, nch * k, st));
         StreamChunkArgs s{};
+        if (t8) {
+            s.t8 = c->st_t8.as<unsigned long long>();
+            s.bb = bb;
+            s.pb = pb;
+            s.fid_bm = c->fid_table.as<uint32_t *>();
+            s.flag = c->st_flag.as<uint8_t>();
+        }
         s.adds = c->st_adds.as<uint32_t>();
         s.nadds = c->st_prefilter.as<uint32_t>() + kPrefilterWords;
         if (g_stream_prefilter) {
@@ -2231,6 +2304,7 @@ static int hll_import(rbx_ctx *c, const std::string &name, const uint8_t *bytes,
     for (int i = 0; i < 8; ++i) card |= (uint64_t)bytes[8 + i] << (8 * i);
     h->card = card;
     h->dense = bytes[4] == 0;  // SET keeps the string's encoding
+    RBX_TRY(hll_ops_reserve(h.get(), ops.size()));
     // state: not promoted, the stored opcodes (a sparse string covers 16384 registers: >= 1)
     const uint32_t st[kHllStateWords] = {0u, (uint32_t)ops.size(), (uint32_t)(len - 16), 0u};
     HIP_TRY(hipMemcpyAsync(h->d_promoted, st, sizeof(st), hipMemcpyHostToDevice, c->stream));
@@ -2638,15 +2712,20 @@ int rbx_bench_slice_probe(rbx_ctx *c, const void *d_entries, uint64_t per_bucket
     return RBX_OK;
 }
 
+static int quiesce(rbx_ctx *c);
 int rbx_bench_add_stamps(rbx_ctx *c, unsigned long long *out, uint32_t n) {
     if (!c || !out || n > 16) return fail(RBX_E_ILLEGAL_ARGUMENT, "rbx_bench_add_stamps: n <= 16");
+    // the context's lock and device, and only this context's work drained
+    std::lock_guard<std::recursive_mutex> g(c->ks.mu);
+    RBX_TRY(set_device(c));  // fails on a shut context (pa_stamps freed)
     if (c->pa_stamps.cap == 0) {
         memset(out, 0, n * 8);
         return RBX_OK;
     }
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(out, c->pa_stamps.p, n * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemset(c->pa_stamps.p, 0, 16 * 8));
+    RBX_TRY(quiesce(c));
+    HIP_TRY(hipMemcpyAsync(out, c->pa_stamps.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemsetAsync(c->pa_stamps.p, 0, 16 * 8, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return RBX_OK;
 }
 
@@ -2907,9 +2986,16 @@ int rbx_hll_copy_to(rbx_ctx *src, rbx_name src_name, rbx_ctx *dst, rbx_name dst_
     }
     h->card = sh->card;
     h->dense = sh->dense;
+    // the source's opcode count (its state word [1]) sizes the copy and the destination's list
+    uint32_t sst[kHllStateWords];
+    HIP_TRY(hipSetDevice(src->device));
+    HIP_TRY(hipMemcpy(sst, sh->d_promoted, sizeof(sst), hipMemcpyDeviceToHost));
+    HIP_TRY(hipSetDevice(dst->device));
+    RBX_TRY(hll_ops_reserve(h.get(), sst[1]));
     HIP_TRY(hipMemcpyPeerAsync(h->d_regs, dst->device, sh->d_regs, src->device, kHllBytes, dst->stream));
     HIP_TRY(hipMemcpyPeerAsync(h->d_promoted, dst->device, sh->d_promoted, src->device, kHllStateWords * 4, dst->stream));
-    HIP_TRY(hipMemcpyPeerAsync(h->d_sp_ops, dst->device, sh->d_sp_ops, src->device, kHllOpsBytes, dst->stream));
+    if (sst[1])
+        HIP_TRY(hipMemcpyPeerAsync(h->d_sp_ops, dst->device, sh->d_sp_ops, src->device, (size_t)sst[1] * 2, dst->stream));
     HIP_TRY(hipStreamSynchronize(dst->stream));
     return RBX_OK;
 }
@@ -2974,6 +3060,11 @@ int rbx_tune(const char *key, int value) {
         if (value != 22 && value != 24 && value != 32 && value != 34 && value != 42 && value != 44)
             return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qshape in {22, 24, 32, 34, 42, 44}");
         set_contains_qshape(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_table8")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_table8 is 0 or 1");
+        g_stream_table8 = value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_chunk")) {

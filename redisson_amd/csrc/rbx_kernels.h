@@ -164,7 +164,23 @@ struct StreamChunkArgs {
     uint32_t *nadds;      // 1, zeroed per chunk
     uint32_t *prefilter;  // 2^pbits bits, zeroed per chunk; null: no prefilter (rbx_tune stream_prefilter 0)
     uint32_t pshift;      // 64 - pbits
+    // r04 first-setter table of 8-byte entries (null: the 16-byte epoch-tagged `table` above).
+    // entry = (fid << bb | bit) << pb | chunk position, EMPTY = ~0; one CAS claims a bit, and an
+    // atomicMin keeps the first setter of a shared one.  Capacity 2^t8_log2(*nadds, kmax), from the
+    // chunk's add count on the device; k_stream_walk commits it and restores every entry to EMPTY.
+    unsigned long long *t8;
+    uint32_t bb, pb;              // bits of the largest bitmap's bit index / of a chunk position
+    uint32_t *const *fid_bm;      // bitmap words per table id (fid)
+    uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks)
 };
+// entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)
+__host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
+    const uint64_t need = (uint64_t)nadds * kmax;
+    const uint64_t want = need + need / 8;
+    uint32_t lg = 12;
+    while ((1ULL << lg) < want) ++lg;
+    return lg;
+}
 
 // bloom_kernels.hip
 void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st);
@@ -225,7 +241,7 @@ void launch_hll_union(uint8_t *const *d_srcs, uint32_t nsrc, uint8_t *out, hipSt
 // hllSparseSet, replayed in command order): one u16 per opcode -- ZERO and VAL opcodes are their
 // byte, XZERO is (byte0 << 8 | byte1) -- so ZERO < 0x40 <= VAL < 0x100 <= XZERO.
 struct HllReplay {
-    uint16_t *ops;        // the HLL's opcode list (16384 entries of capacity)
+    uint16_t *ops;        // the HLL's opcode list (capacity >= max(its bytes, 3000): opcodes <= bytes)
     uint32_t *state;      // [0] promoted (sticky: the list is stale once set), [1] opcodes (0 = the
                           // createHLLObject string, one XZERO), [2] opcode bytes (after the header)
     const uint8_t *regs;  // merge mode (PFMERGE write-back): the max registers, ascending; else null

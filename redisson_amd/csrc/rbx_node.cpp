@@ -11,15 +11,18 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/rbx.h"
+#include "../../include/rbx_bench.h"
 #include "keyspace.h"
 
 using namespace rbx;
@@ -47,6 +50,13 @@ struct rbx_node {
     // contains are spread over them (Redisson's ReadMode.SLAVE reads,
     // M/config/BaseMasterSlaveServersConfig.java:60; GETBIT is a read, M/RedissonBitSet.java:277-279)
     std::set<std::string> replicated;
+    // Replication barrier: a batch holds it shared from the moment it reads `replicated` until its
+    // kernels are done; replicate(on / off), DEL, and dropping the copies after a failed replicated
+    // add hold it exclusively.  So a replica copy never misses an add that ran during the copy, and
+    // copies are never deleted under a contains already routed to them.
+    std::shared_mutex repl_mu;
+    // test hook (rbx_node_test_fail_adds): the next fail_adds[g] Bloom adds on GPU g fail
+    std::unique_ptr<std::atomic<int>[]> fail_adds;
 };
 
 static bool is_replicated(rbx_node *nd, const std::string &name) {
@@ -108,6 +118,8 @@ int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
         for (int j = 0; j < n_gpus; ++j)
             (void)rbx_enable_peer_access(devices ? devices[i] : i, devices ? devices[j] : j);
     auto *nd = new rbx_node();
+    nd->fail_adds.reset(new std::atomic<int>[n_gpus]);
+    for (int i = 0; i < n_gpus; ++i) nd->fail_adds[i] = 0;
     for (int i = 0; i < n_gpus; ++i) {
         rbx_ctx *c = nullptr;
         const int rc = rbx_init(devices ? devices[i] : i, &c);
@@ -173,21 +185,88 @@ static std::vector<int> all_gpus(const rbx_node *nd) {
     return g;
 }
 
+// the test hook: true (and one injected failure used up) when GPU g's next add must fail
+static bool injected_add_fault(rbx_node *nd, int g) {
+    int v = nd->fail_adds[g].load();
+    while (v > 0)
+        if (nd->fail_adds[g].compare_exchange_weak(v, v - 1)) return true;
+    return false;
+}
+
+static int node_add_on(rbx_node *nd, int g, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
+                       uint8_t *out_new, uint64_t *out_count) {
+    if (injected_add_fault(nd, g)) return fail(RBX_E_DEVICE, "injected add fault (rbx_node_test_fail_adds)");
+    return rbx_bloom_add_n(nd->ctx[g], name, size, k, keys, out_new, out_count);
+}
+
+// Failure semantics of a replicated add: when the add failed on any replica, the replicas may
+// differ (a replica that succeeded holds bits another lacks), so the filter stops being
+// replicated.  The caller has already taken the names out of `replicated` (under nd->mu, while
+// it still held the barrier shared, so no later batch is routed to a copy); here, with the
+// barrier exclusive (no batch still running on a copy), the copies on the non-home GPUs are
+// deleted and their cached handles evicted.  The home GPU keeps the filter as its own add left
+// it, and the caller returns the add's error.  A name replicated again meanwhile is left alone.
+static void drop_copies_locked(rbx_node *nd, const std::string &nm) {
+    const int home = gpu_of(nd, nm);
+    const std::string cn = config_name(nm);
+    const rbx_name both[2] = {name_ref(nm), name_ref(cn)};
+    std::vector<HandleRef> evicted;
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        for (int g = 0; g < (int)nd->ctx.size(); ++g) {
+            if (g == home) continue;
+            auto it = nd->blooms.find(std::make_pair(g, nm));
+            if (it != nd->blooms.end()) {
+                evicted.push_back(std::move(it->second));
+                nd->blooms.erase(it);
+            }
+        }
+    }
+    evicted.clear();  // outside the cache lock: closing takes the context lock
+    for (int g = 0; g < (int)nd->ctx.size(); ++g) {
+        if (g == home) continue;
+        int d;
+        (void)rbx_del_n(nd->ctx[g], both, 2, &d);
+    }
+}
+
+static void drop_replicas_after_failure(rbx_node *nd, const std::vector<std::string> &names) {
+    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
+    for (const std::string &nm : names) {
+        {
+            std::lock_guard<std::mutex> lk(nd->mu);
+            if (nd->replicated.count(nm)) continue;  // replicated again since: its copies are fresh
+        }
+        drop_copies_locked(nd, nm);
+    }
+}
+
 // A replicated filter's add is applied to every replica (the same batch in the same order on
-// each, so they stay identical); the reply is the home GPU's.
+// each, so they stay identical); the reply is the home GPU's.  If any replica fails, the filter
+// is unreplicated (drop_replicas_after_failure) and the first error (in GPU order) is returned.
 int rbx_node_bloom_add(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, const rbx_keys *keys,
                        uint8_t *out_new, uint64_t *out_count) {
     if (!nd) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL node");
     NODE_TRY(check_name(name));
     const std::string nm = str_of(name);
     const int home = gpu_of(nd, nm);
-    if (!is_replicated(nd, nm) || nd->ctx.size() == 1)
-        return rbx_bloom_add_n(nd->ctx[home], name, size, k, keys, out_new, out_count);
-    return per_gpu(all_gpus(nd), [&](int g) -> int {
-        uint64_t cnt = 0;
-        return rbx_bloom_add_n(nd->ctx[g], name, size, k, keys, g == home ? out_new : nullptr,
+    int rc;
+    {
+        std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
+        if (!is_replicated(nd, nm) || nd->ctx.size() == 1)
+            return node_add_on(nd, home, name, size, k, keys, out_new, out_count);
+        rc = per_gpu(all_gpus(nd), [&](int g) -> int {
+            uint64_t cnt = 0;
+            return node_add_on(nd, g, name, size, k, keys, g == home ? out_new : nullptr,
                                g == home ? out_count : &cnt);
-    });
+        });
+        if (rc == RBX_OK) return RBX_OK;
+        std::lock_guard<std::mutex> lk(nd->mu);
+        nd->replicated.erase(nm);
+    }
+    const std::string msg = rbx_last_error();
+    drop_replicas_after_failure(nd, {nm});
+    return fail(rc, msg);
 }
 
 // A replicated filter's contains is split into one contiguous key range per replica, run
@@ -199,6 +278,7 @@ int rbx_node_bloom_contains(rbx_node *nd, rbx_name name, uint64_t size, uint32_t
     const std::string nm = str_of(name);
     const int home = gpu_of(nd, nm);
     const uint64_t N = nd->ctx.size();
+    std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
     if (!keys || keys->n < N || !is_replicated(nd, nm) || N == 1)
         return rbx_bloom_contains_n(nd->ctx[home], name, size, k, keys, out_present, out_count);
     if (keys->n && !keys->bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
@@ -229,10 +309,22 @@ int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
     std::vector<int> others;
     for (int g = 0; g < (int)nd->ctx.size(); ++g)
         if (g != home) others.push_back(g);
+    // exclusive: no add runs between the copy and the routing change, and no contains still runs on
+    // a copy when it is deleted
+    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
     if (on) {
         rbx_bloom_config cfg;
         NODE_TRY(rbx_bloom_read_config_n(nd->ctx[home], name, &cfg));  // not initialized: ISE
-        NODE_TRY(per_gpu(others, [&](int g) -> int { return rbx_bloom_copy_to(nd->ctx[home], nd->ctx[g], name); }));
+        const int rc = per_gpu(others, [&](int g) -> int { return rbx_bloom_copy_to(nd->ctx[home], nd->ctx[g], name); });
+        if (rc != RBX_OK) {  // a partial copy (or re-sync) is not a replica: drop whatever landed
+            const std::string msg = rbx_last_error();
+            {
+                std::lock_guard<std::mutex> lk(nd->mu);
+                nd->replicated.erase(nm);
+            }
+            drop_copies_locked(nd, nm);
+            return fail(rc, msg);
+        }
         std::lock_guard<std::mutex> lk(nd->mu);
         nd->replicated.insert(nm);
         return RBX_OK;
@@ -242,10 +334,28 @@ int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
         nd->replicated.erase(nm);
     }
     const rbx_name both[2] = {name, name_ref(cn)};
+    std::vector<HandleRef> evicted;
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        for (int g : others) {
+            auto it = nd->blooms.find(std::make_pair(g, nm));
+            if (it != nd->blooms.end()) {
+                evicted.push_back(std::move(it->second));
+                nd->blooms.erase(it);
+            }
+        }
+    }
+    evicted.clear();
     return per_gpu(others, [&](int g) -> int {
         int d;
         return rbx_del_n(nd->ctx[g], both, 2, &d);
     });
+}
+
+int rbx_node_test_fail_adds(rbx_node *nd, int gpu, int n) {
+    if (!nd || gpu < 0 || gpu >= (int)nd->ctx.size() || n < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "bad argument");
+    nd->fail_adds[gpu] = n;
+    return RBX_OK;
 }
 
 int rbx_node_bloom_is_replicated(rbx_node *nd, rbx_name name, int *out) {
@@ -279,19 +389,31 @@ static std::vector<std::string> filters_of(const std::string &key) {
 
 int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) {
     if (!nd || (n && !names)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    for (uint32_t i = 0; i < n; ++i) NODE_TRY(check_name(names[i]));
+    // exclusive: no batch still runs on a copy being deleted
+    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
     std::vector<std::vector<rbx_name>> by(nd->ctx.size());
     std::vector<std::vector<rbx_name>> replica_keys(nd->ctx.size());  // copies: not counted
+    std::deque<std::string> held;  // names the replica deletions add (a config's filter bitmap)
+    std::vector<std::string> evict;
     for (uint32_t i = 0; i < n; ++i) {
-        NODE_TRY(check_name(names[i]));
         const std::string key = str_of(names[i]);
         const int home = gpu_of(nd, key);
         by[home].push_back(names[i]);
+        evict.push_back(key);
         std::lock_guard<std::mutex> lk(nd->mu);
         bool repl = false;
         for (const std::string &f : filters_of(key)) {
             if (!nd->replicated.count(f)) continue;
             repl = true;
-            if (f != key) nd->replicated.erase(f);  // the config is gone: the filter is gone
+            if (f == key) continue;
+            // the config is gone: the filter is gone, and so are its copies -- the bitmap copies too,
+            // whatever the order of the names (a config-only DEL left 512 MiB orphans)
+            nd->replicated.erase(f);
+            held.push_back(f);
+            evict.push_back(f);
+            for (size_t g = 0; g < nd->ctx.size(); ++g)
+                if ((int)g != home) replica_keys[g].push_back(name_ref(held.back()));
         }
         if (repl)
             for (size_t g = 0; g < nd->ctx.size(); ++g)
@@ -301,9 +423,9 @@ int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) 
     std::vector<HandleRef> evicted;
     {
         std::lock_guard<std::mutex> lk(nd->mu);
-        for (uint32_t i = 0; i < n; ++i) {
+        for (const std::string &nm : evict) {
             for (int g = 0; g < (int)nd->ctx.size(); ++g) {  // replicas are cached on every GPU
-                auto it = nd->blooms.find(std::make_pair(g, str_of(names[i])));
+                auto it = nd->blooms.find(std::make_pair(g, nm));
                 if (it != nd->blooms.end()) {
                     evicted.push_back(std::move(it->second));
                     nd->blooms.erase(it);
@@ -440,30 +562,48 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
     std::vector<std::string> sn(nseg);
     for (uint32_t s = 0; s < nseg; ++s) sn[s] = str_of(names[s]);
     std::vector<uint8_t> repl(nseg, 0);
-    {
-        std::lock_guard<std::mutex> lk(nd->mu);
-        if (!nd->replicated.empty())
-            for (uint32_t s = 0; s < nseg; ++s) repl[s] = nd->replicated.count(sn[s]) != 0;
-    }
     std::vector<Part> parts;
-    build_parts(nd, sn, seg, keys, &parts, &repl, is_add);
-    const std::vector<int> gpus = gpus_with_work(parts);
-    const int rc = per_gpu(gpus, [&](int g) -> int {
-        Part &p = parts[g];
-        for (int attempt = 0;; ++attempt) {
-            std::vector<HandleRef> refs(p.segs.size());  // held for the batch
-            std::vector<rbx_bloom *> hs(p.segs.size());
-            for (size_t j = 0; j < p.segs.size(); ++j) {
-                NODE_TRY(bloom_handle(nd, g, sn[p.segs[j]], attempt > 0, &refs[j]));
-                hs[j] = refs[j]->h;
-            }
-            const auto fn = is_add ? rbx_bloom_add_multi : rbx_bloom_contains_multi;
-            const int r = fn(nd->ctx[g], hs.data(), (uint32_t)hs.size(), p.seg.data(), &p.keys,
-                             out ? p.out.data() : nullptr, p.cnt.data());
-            if (r != RBX_E_CONFIG_CHANGED || attempt > 0) return r;
+    std::vector<int> gpus;
+    std::vector<std::string> unreplicated;  // replicated names of a failed add
+    int rc;
+    {
+        std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
+        {
+            std::lock_guard<std::mutex> lk(nd->mu);
+            if (!nd->replicated.empty())
+                for (uint32_t s = 0; s < nseg; ++s) repl[s] = nd->replicated.count(sn[s]) != 0;
         }
-    });
-    if (rc != RBX_OK) return rc;
+        build_parts(nd, sn, seg, keys, &parts, &repl, is_add);
+        gpus = gpus_with_work(parts);
+        rc = per_gpu(gpus, [&](int g) -> int {
+            Part &p = parts[g];
+            if (is_add && injected_add_fault(nd, g)) return fail(RBX_E_DEVICE, "injected add fault (rbx_node_test_fail_adds)");
+            for (int attempt = 0;; ++attempt) {
+                std::vector<HandleRef> refs(p.segs.size());  // held for the batch
+                std::vector<rbx_bloom *> hs(p.segs.size());
+                for (size_t j = 0; j < p.segs.size(); ++j) {
+                    NODE_TRY(bloom_handle(nd, g, sn[p.segs[j]], attempt > 0, &refs[j]));
+                    hs[j] = refs[j]->h;
+                }
+                const auto fn = is_add ? rbx_bloom_add_multi : rbx_bloom_contains_multi;
+                const int r = fn(nd->ctx[g], hs.data(), (uint32_t)hs.size(), p.seg.data(), &p.keys,
+                                 out ? p.out.data() : nullptr, p.cnt.data());
+                if (r != RBX_E_CONFIG_CHANGED || attempt > 0) return r;
+            }
+        });
+        // a failed add may have reached some replicas of a replicated filter and not others: every
+        // replicated filter of the batch stops being replicated (see drop_replicas_after_failure)
+        if (rc != RBX_OK && is_add) {
+            std::lock_guard<std::mutex> lk(nd->mu);
+            for (uint32_t s = 0; s < nseg; ++s)
+                if (repl[s] && nd->replicated.erase(sn[s])) unreplicated.push_back(sn[s]);
+        }
+    }
+    if (rc != RBX_OK) {
+        const std::string msg = rbx_last_error();
+        if (!unreplicated.empty()) drop_replicas_after_failure(nd, unreplicated);
+        return fail(rc, msg);
+    }
     // gather in segment order
     for (int g : gpus) {
         const Part &p = parts[g];

@@ -30,7 +30,7 @@ def _zipf_tenants(rng, nt, n, s=1.0):
     return np.minimum(np.searchsorted(cdf, rng.random(n)), nt - 1).astype(np.uint32)
 
 
-def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None):
+def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None):
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
@@ -46,6 +46,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         refs.append(r)
         handles.append(BloomHandle(client, nm))
     kf = _zipf_tenants(rng, nt, n)
+    if nt > 1 << 16:  # ids past 2^16 (the tag's filter-id field, the prefilter hash) really occur
+        assert int(kf.max()) >= 1 << 16 and np.count_nonzero(kf >= 1 << 8) > n // 4
     op = (rng.random(n) < 0.1).astype(np.uint8)
     pool = rng.integers(0, 256, size=(n // 4, klen), dtype=np.uint8)
     keys = pool[rng.integers(0, len(pool), size=n)]
@@ -59,12 +61,15 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
     if prefilter is not None:
         assert L.lib().rbx_tune(b"stream_prefilter", prefilter) == 0
+    if table8 is not None:
+        assert L.lib().rbx_tune(b"stream_table8", table8) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
     finally:
         L.lib().rbx_tune(b"stream_chunk", 0)
         L.lib().rbx_tune(b"stream_contains_slots", STREAM_SLOTS_DEFAULT)
         L.lib().rbx_tune(b"stream_prefilter", STREAM_PREFILTER_DEFAULT)
+        L.lib().rbx_tune(b"stream_table8", 1)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -106,8 +111,33 @@ def test_c5_kmax8_many_chunks(client, fresh, slots, prefilter):
              chunk=300_000, slots=slots, prefilter=prefilter)
 
 
+@pytest.mark.parametrize("table8", [0, 1])
+def test_c5_first_setter_tables_agree(client, fresh, table8):
+    """The r03 16-byte epoch-tagged first-setter table (stream_table8 0) and the r04 8-byte table with
+    the walk commit (1, default) on the same C5-shaped stream: both must equal the oracle."""
+    _c5_case(client, fresh, seed=4242, nt=300, expected=1_000_000, fpp=1e-3, n=1_500_000, chunk=500_000,
+             table8=table8)
+
+
 def test_c5_k10_chunk_boundaries(client, fresh):
     """C5 tenants and keys in 303,031-command chunks (= 101 * 3000 + 1: the add at 303,030 and the
     contains of the same key at 303,031 sit on the two sides of the first boundary; the earlier
     chunk's commit must land before the next chunk probes)."""
     _c5_case(client, fresh, seed=91, nt=100, expected=1_000_000, fpp=1e-3, n=2_000_000, chunk=303_031)
+
+
+@pytest.mark.parametrize("prefilter", [23, 0])
+def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, prefilter):
+    """C5's tenant count.  The first-setter tags and the prefilter hash carry the
+    filter's index in the call (up to 2^17 here), so the bench leg's id range is checked against the
+    oracle too: 100,000 tryInit(1000, 1e-3) tenants (14,378 bits, k = 10 -> the same <64, 16>
+    instantiation as C5, 1.8 KB each), Zipf(1.0) tenants, 10% adds, 64-byte keys, 2.1M commands in
+    three chunks, with the prefilter (default 2^23 bits) and without it (every clear bit looked up in
+    the table).  Per-command replies, both counts and every tenant's bitmap must be identical."""
+    f = client.getBloomFilter(fresh + "-probe")
+    f.tryInit(1000, 1e-3)
+    assert (f.getSize(), f.getHashIterations()) == (14_378, 10)
+    f.delete()
+    wc = _c5_case(client, fresh, seed=0xC5100 + prefilter, nt=100_000, expected=1000, fpp=1e-3, n=2_100_000,
+                  chunk=700_000, prefilter=prefilter)
+    assert wc[1] > 10_000

@@ -361,3 +361,136 @@ def test_cross_gpu_hll_union_keeps_encodings(node, fresh):
     assert s2[4] == 0 and np.array_equal(O.hll_dense_unpack(s2[16:]), u)  # dense
     assert node.getHyperLogLog(names[0]).countWith(*names[1:]) == O.hll_count(u)
     assert node.delete(*names, d1, d2) == len(names) + 2
+
+
+def _exists_anywhere(node, names):
+    import ctypes as C
+
+    out = []
+    for g in range(N):
+        e = C.c_int()
+        arr, keep = L.names_array(names)
+        assert L.lib().rbx_exists_n(_ctx(node, g), arr, len(names), C.byref(e)) == 0
+        out.append(e.value)
+    return out
+
+
+def test_replicated_add_failure_drops_replication(node, fresh):
+    """an add of a replicated filter that fails on one replica must not leave the
+    copies divergent and still marked replicated.  The node then drops the replication: the copies
+    are deleted on every non-home GPU, contains go to the home GPU, and the error is returned.  A
+    test hook (rbx_node_test_fail_adds) fails the next add on a chosen GPU before it runs."""
+    from redisson_amd.exceptions import DeviceError
+
+    rng = np.random.default_rng(47)
+    nm, other = fresh + "-rf", fresh + "-rf-other"
+    f = node.getBloomFilter(nm)
+    assert f.tryInit(100_000, 0.01)
+    ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+    nbytes = (f.getSize() + 7) // 8
+    home = node.gpu_of(nm)
+    k1 = [rng.bytes(20) for _ in range(5000)]
+    assert f.add(k1) == ref.add(*O.arena(k1))
+    f.replicate()
+    # a replica (not the home GPU) fails: home applied the add, the copies are dropped
+    victim = (home + 1) % N
+    assert L.lib().rbx_node_test_fail_adds(node.node, victim, 1) == 0
+    k2 = [rng.bytes(20) for _ in range(5000)]
+    with pytest.raises(DeviceError, match="injected"):
+        f.add(k2)
+    ref.add(*O.arena(k2))
+    assert not f.isReplicated()
+    assert _export(_ctx(node, home), nm, nbytes) == ref.redis_string()
+    ex = _exists_anywhere(node, [nm, "{" + nm + "}:config"])
+    assert ex[home] == 2 and all(ex[g] == 0 for g in range(N) if g != home), ex
+    probe = k1[:1000] + k2[:1000] + [rng.bytes(20) for _ in range(3000)]
+    cp, pres = f.containsEach(probe)
+    crp, pr = ref.contains(*O.arena(probe), per_key=True)
+    assert cp == crp and np.array_equal(pres, pr)
+    # the home GPU fails inside a multi-tenant batch: the replicas applied it, home did not -- the
+    # replication is dropped again and home keeps its own (unchanged) filter
+    assert node.getBloomFilter(other).tryInit(10_000, 0.01)
+    f.replicate()
+    assert f.isReplicated()
+    assert L.lib().rbx_node_test_fail_adds(node.node, home, 1) == 0
+    k3 = [rng.bytes(16) for _ in range(2000)]
+    with pytest.raises(DeviceError, match="injected"):
+        node.bloom_add_multi([nm, other], [0, 1000, 2000], Arena(k3))
+    assert L.lib().rbx_node_test_fail_adds(node.node, home, 0) == 0
+    assert not f.isReplicated()
+    assert _export(_ctx(node, home), nm, nbytes) == ref.redis_string()
+    ex = _exists_anywhere(node, [nm, "{" + nm + "}:config"])
+    assert all(ex[g] == 0 for g in range(N) if g != home), ex
+    # replicated again, everything agrees
+    f.replicate()
+    for g in range(N):
+        assert _export(_ctx(node, g), nm, nbytes) == ref.redis_string(), g
+    # `other` got its bitmap unless its part of the batch ran on the failed (home) GPU
+    other_bm = _exists_anywhere(node, [other])[node.gpu_of(other)]
+    assert other_bm == (0 if node.gpu_of(other) == home else 1)
+    assert node.delete(nm, "{" + nm + "}:config", other, "{" + other + "}:config") == 3 + other_bm
+
+
+def test_replicate_concurrent_with_adds(node, fresh):
+    """replicate(on) concurrent with adds of the same filter.  The copy and the
+    routing change are exclusive against batches, so no add reaches only the home GPU: afterwards
+    every replica equals the oracle's bitmap, and every added key is present through each replica."""
+    import threading
+
+    rng = np.random.default_rng(48)
+    nm = fresh + "-rc"
+    f = node.getBloomFilter(nm)
+    assert f.tryInit(400_000, 0.01)
+    ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+    nbytes = (f.getSize() + 7) // 8
+    batches = [[rng.bytes(24) for _ in range(4000)] for _ in range(40)]
+    errors = []
+
+    def adder():
+        try:
+            for b in batches:
+                f.add(b)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    t = threading.Thread(target=adder)
+    t.start()
+    f.replicate()
+    t.join()
+    assert not errors, errors
+    for b in batches:
+        ref.add(*O.arena(b))
+    want = ref.redis_string()
+    for g in range(N):
+        assert _export(_ctx(node, g), nm, nbytes) == want, g
+    allk = [k for b in batches for k in b]
+    assert f.contains(allk) == len(allk)  # spread over the replicas
+    # and replicate(off) concurrent with contains: the answers never lose a key
+    res = []
+
+    def checker():
+        for _ in range(10):
+            res.append(f.contains(allk[:20_000]))
+
+    t = threading.Thread(target=checker)
+    t.start()
+    f.replicate(False)
+    t.join()
+    assert res == [20_000] * 10
+    node.delete(nm, "{" + nm + "}:config")
+
+
+def test_config_only_delete_drops_replica_bitmaps(node, fresh):
+    """DEL of only a replicated filter's config ends the replication and deletes the
+    copies' bitmaps too (Redis keeps the home bitmap; the copies are the node's own)."""
+    nm = fresh + "-cd"
+    f = node.getBloomFilter(nm)
+    assert f.tryInit(50_000, 0.01)
+    f.add([b"a", b"b"])
+    f.replicate()
+    home = node.gpu_of(nm)
+    assert node.delete("{" + nm + "}:config") == 1
+    assert not f.isReplicated()
+    ex = _exists_anywhere(node, [nm, "{" + nm + "}:config"])
+    assert ex[home] == 1 and all(ex[g] == 0 for g in range(N) if g != home), ex
+    assert node.delete(nm) == 1
