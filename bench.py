@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--tune", default="", help="extra rbx_tune settings for experiments: key=value,key=value")
     p.add_argument("--zipf-s", type=float, default=1.0, help="C5 tenant skew")
     p.add_argument("--add-fraction", type=float, default=0.1, help="C5 share of add commands")
+    p.add_argument("--c5-replies", type=int, default=1,
+                   help="C5: write every command's reply in the timed step (1, the metric) or not (0, A/B only)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline C2 sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-hostpath", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -782,7 +784,8 @@ def run_c5(args, world, rank, local, steps, warmup):
 
     def step():
         assert L.lib().rbx_bloom_stream_dev(client.ctx, arr, nt, kf.data_ptr(), op.data_ptr(), C.byref(dk),
-                                             replies.data_ptr(), counts.data_ptr(), sptr) == 0
+                                             replies.data_ptr() if args.c5_replies else None, counts.data_ptr(),
+                                             sptr) == 0
 
     for _ in range(warmup):
         step()
@@ -815,7 +818,8 @@ def run_c5(args, world, rank, local, steps, warmup):
                                f"{nt} tenant filters tryInit(1e6,1e-3) at design fill, Zipf(s={args.zipf_s}) tenants, "
                                "64-byte keys, in-order semantics",
                    "tenants_this_gpu": nt, "ops_per_gpu": n, "hottest_tenant_ops": top,
-                   "replies": "one u8 reply per command written to HBM in every timed step",
+                   "replies": "one u8 reply per command written to HBM in every timed step" if args.c5_replies
+                   else "NOT written (A/B run; not the metric)",
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
@@ -973,6 +977,9 @@ def main():
         from redisson_amd import _lib as L
 
         key, val = kv.split("=")
+        if key == "c5_replies":  # bench-side A/B switch (not an engine knob): C5 timed without replies
+            args.c5_replies = int(val)
+            continue
         assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
     log(f"[bench] rank {rank}/{world} workload {args.workload}")
     if args.dry_run:

@@ -1539,6 +1539,8 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     KeysDev keys = keys_dev(d_keys);
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, (1ULL << 26) / k));
+    // chunk bases on 128-command boundaries keep the replies' range images line-aligned
+    if (chunk < keys.n && chunk > 128) chunk &= ~127ULL;
     if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_adds.reserve(chunk * 4));
@@ -1553,7 +1555,8 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     const bool t8 = g_stream_table8 && bb + fbits <= 41;
     const uint32_t pb = 64 - bb - fbits;
     if (t8) {
-        chunk = std::min<uint64_t>(chunk, std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, 1ULL << 30));
+        const uint64_t cap = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, 1ULL << 30);
+        if (chunk > cap) chunk = cap > 128 ? cap & ~127ULL : cap;
         const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)k);
         if (c->st_t8_entries < entries) {
             c->st_t8_entries = 0;

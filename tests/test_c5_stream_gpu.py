@@ -130,13 +130,13 @@ def test_c5_k10_chunk_boundaries(client, fresh):
 def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, prefilter):
     """C5's tenant count.  The first-setter tags and the prefilter hash carry the
     filter's index in the call (up to 2^17 here), so the bench leg's id range is checked against the
-    oracle too: 100,000 tryInit(1000, 1e-3) tenants (14,378 bits, k = 10 -> the same <64, 16>
+    oracle too: 100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10 -> the same <64, 16>
     instantiation as C5, 1.8 KB each), Zipf(1.0) tenants, 10% adds, 64-byte keys, 2.1M commands in
     three chunks, with the prefilter (default 2^23 bits) and without it (every clear bit looked up in
     the table).  Per-command replies, both counts and every tenant's bitmap must be identical."""
     f = client.getBloomFilter(fresh + "-probe")
     f.tryInit(1000, 1e-3)
-    assert (f.getSize(), f.getHashIterations()) == (14_378, 10)
+    assert (f.getSize(), f.getHashIterations()) == (14_377, 10)
     f.delete()
     wc = _c5_case(client, fresh, seed=0xC5100 + prefilter, nt=100_000, expected=1000, fpp=1e-3, n=2_100_000,
                   chunk=700_000, prefilter=prefilter)

@@ -31,7 +31,9 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
          ("k_bk_misses", r"k_bk_misses"), ("k_bk_final", r"k_bk_final"), ("k_stream_compact", r"k_stream_compact"),
          ("k_ba_stage1", r"k_ba_stage1<"), ("k_ba_rebucket", r"k_ba_rebucket"), ("k_ba_region", r"k_ba_region"),
          ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
-         ("k_stream_probe", r"k_stream_probe<"), ("k_stream_contains_q", r"k_stream_contains_q<"),
+         ("k_stream_probe", r"k_stream_probe<"), ("k_stream_probe8", r"k_stream_probe8<"),
+         ("k_stream_walk", r"k_stream_walk"), ("k_stream_final", r"k_stream_final"),
+         ("k_stream_contains_q", r"k_stream_contains_q<"),
          ("k_stream_contains", r"k_stream_contains<"),
          ("k_stream_commit", r"k_stream_commit<"),
          ("k_bloom_contains_multi", r"k_bloom_contains_multi<"), ("k_bloom_contains_q", r"k_bloom_contains_q<"),
@@ -44,7 +46,7 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
 CLASS = {"k_bk_stage1": "mixed", "k_bloom_contains": "mixed", "k_bloom_contains_multi": "mixed",
          "k_bloom_contains_q": "mixed", "k_stream_probe": "mixed", "k_stream_contains": "mixed",
          "k_stream_contains_q": "mixed",
-         "k_stream_commit": "mixed", "k_gather_probe": "gather", "k_bloom_add_probe": "gather",
+         "k_stream_commit": "mixed", "k_stream_probe8": "mixed", "k_gather_probe": "gather", "k_bloom_add_probe": "gather",
          "k_bloom_add_commit": "gather"}  # every other kernel: stream
 
 
@@ -104,6 +106,12 @@ def main():
             e["requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"] + cs["TCC_EA0_WRREQ_sum"]
             e["read_requests_per_launch"] = cs["TCC_EA0_RDREQ_sum"]
             e["write_requests_per_launch"] = cs["TCC_EA0_WRREQ_sum"]
+        if "TCC_ATOMIC_sum" in cs:
+            # atomic requests at the L2 (all types), and those sent on to memory (EA): the atomic
+            # throughput north_star asks for; EA atomics also count in TCC_EA0_WRREQ
+            e["atomic_requests_per_launch"] = cs["TCC_ATOMIC_sum"]
+        if "TCC_EA0_ATOMIC_sum" in cs:
+            e["ea_atomic_requests_per_launch"] = cs["TCC_EA0_ATOMIC_sum"]
         rd = cs.get("TCC_EA0_RDREQ_sum")
         if rd is None and fetch is not None:
             rd = fetch * 1024 / 64  # FETCH_SIZE = RDREQ x 64 B
@@ -127,8 +135,9 @@ def main():
     # all profiled launches' counters / the calls in the profiled run (--calls)
     for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_misses", "k_bk_final")),
                         ("add_pipeline", ("k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys", "k_ba_final")),
-                        ("stream_pipeline", ("k_stream_compact", "k_stream_probe", "k_stream_contains", "k_stream_contains_q",
-                                             "k_stream_commit"))):
+                        ("stream_pipeline", ("k_stream_compact", "k_stream_probe", "k_stream_probe8", "k_stream_contains",
+                                             "k_stream_contains_q", "k_stream_commit", "k_stream_walk",
+                                             "k_stream_final"))):
         # the stream pipeline runs one of its two contains kernels (staged or slot)
         parts = tuple(k for k in parts if k in out)
         if len(parts) < 3 or name not in calls:
@@ -137,7 +146,8 @@ def main():
                "note": "per API call: sum over the profiled launches / calls (the keys "
                        "written '_per_launch' here mean per call)"}
         for f in ("hbm_bytes_per_launch", "hbm_bytes_by_class", "requests_per_launch", "read_requests_per_launch",
-                  "write_requests_per_launch", "fetch_bytes_x2", "write_bytes"):
+                  "write_requests_per_launch", "fetch_bytes_x2", "write_bytes", "atomic_requests_per_launch",
+                  "ea_atomic_requests_per_launch"):
             if all(f in out[k] for k in parts):
                 agg[f] = sum(out[k][f] * launches[k] for k in parts) / calls[name]
         out[name] = agg
