@@ -380,7 +380,8 @@ __device__ __forceinline__ uint32_t block_scan(Lds &L, uint32_t v, uint32_t &exc
 // into fresh keys costs a register scan, not an element-by-element walk.  Thread t scans
 // registers [64t, 64t + 64); a run is charged by the thread holding its first register, which
 // finds the run's end through a suffix minimum of the threads' first run starts.
-__device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes) {
+__device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes, uint64_t canon_max_bytes,
+                             bool &canon) {
     const uint32_t t = threadIdx.x, base = t * 64;
     const uint32_t *w = (const uint32_t *)(regs + base);  // the thread's 64 registers, a word at a time
     uint32_t p = t ? regs[base - 1] : 0xffffffffu;
@@ -407,28 +408,109 @@ __device__ bool must_promote(sp::Lds &L, const uint8_t *regs, uint64_t max_bytes
         __syncthreads();
     }
     const uint32_t next_after = t + 1 < 256 ? s_first[t + 1] : 16384u;
-    uint32_t bytes = 0;
+    // bytes: the fewest-bytes encoding; bbound: B = the zero runs' bytes + one byte per nonzero
+    // register (no string of these registers is longer); longrun: a nonzero run longer than 4
+    uint32_t bytes = 0, bbound = 0, longrun = 0;
     for (uint64_t m = starts; m; m &= m - 1) {
         const uint32_t j = (uint32_t)__builtin_ctzll(m);
         const uint64_t later = m & (m - 1);
         const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
         const uint32_t len = end - (base + j), v = regs[base + j];  // (cached: read above)
         bytes += v == 0 ? (len > 64 ? 2u : 1u) : (len + 3) / 4;
+        bbound += v == 0 ? (len > 64 ? 2u : 1u) : len;
+        longrun |= v != 0 && len > 4;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         bytes += __shfl_down(bytes, off, 64);
+        bbound += __shfl_down(bbound, off, 64);
+        longrun |= __shfl_down(longrun, off, 64);
         vmax = max(vmax, (uint32_t)__shfl_down(vmax, off, 64));
     }
     if ((t & 63) == 0) {
         L.part[t >> 6] = bytes;
         L.part[4 + (t >> 6)] = vmax;
+        L.part[8 + (t >> 6)] = bbound;
+        L.part[12 + (t >> 6)] = longrun;
     }
     __syncthreads();
     const uint32_t total = L.part[0] + L.part[1] + L.part[2] + L.part[3];
     const uint32_t mx = max(max(L.part[4], L.part[5]), max(L.part[6], L.part[7]));
+    const uint32_t bb = L.part[8] + L.part[9] + L.part[10] + L.part[11];
+    const uint32_t lr = L.part[12] | L.part[13] | L.part[14] | L.part[15];
     __syncthreads();  // part[] reuse
+    canon = mx <= 32u && !lr && 16u + (uint64_t)bb <= canon_max_bytes;
     return mx > 32u || 16u + (uint64_t)total > max_bytes;
+}
+
+// The string as it stands is the normalized one (what hll_sparse_pack would give its registers):
+// every zero opcode maximal and canonical (XZERO only past 64 registers) and no two adjacent VALs
+// of one value.  (createHLLObject's XZERO over 16384 registers is.)
+__device__ bool sparse_normalized(sp::Lds &L, const HllReplay &it) {
+    const uint32_t t = threadIdx.x, nent = min(it.state[1], (uint32_t)kHllRegs);
+    const uint32_t per = (nent + 255u) / 256u, e0 = min(t * per, nent), e1 = min(e0 + per, nent);
+    uint32_t bad = 0;
+    for (uint32_t e = e0; e < e1; ++e) {
+        const uint32_t op = it.ops[e];
+        const bool zero = op < 0x40u || op >= 0x100u;
+        if (op >= 0x100u && (op & 0x3fffu) + 1u <= 64u) bad = 1;  // an XZERO a ZERO could hold
+        if (e + 1 < nent) {
+            const uint32_t nx = it.ops[e + 1];
+            const bool nzero = nx < 0x40u || nx >= 0x100u;
+            if (zero && nzero) bad = 1;                                               // zero runs not maximal
+            if (!zero && !nzero && ((op >> 2) & 31u) == ((nx >> 2) & 31u)) bad = 1;  // VALs of one value
+        }
+    }
+    const uint64_t b = __ballot(bad != 0);
+    if ((t & 63) == 0) L.part[t >> 6] = b != 0;
+    __syncthreads();
+    const bool ok = !(L.part[0] | L.part[1] | L.part[2] | L.part[3]);
+    __syncthreads();  // part[] reuse
+    return ok;
+}
+
+// Writes the normalized string of the registers (every run one opcode: all nonzero runs are <= 4
+// long) as the HLL's opcode list and its length words.  Thread t encodes the runs starting in
+// registers [64t, 64t + 64).
+__device__ void sparse_encode_normalized(sp::Lds &L, const uint8_t *regs, uint16_t *ops, uint32_t *state) {
+    const uint32_t t = threadIdx.x, base = t * 64;
+    uint32_t p = t ? regs[base - 1] : 0xffffffffu;
+    uint64_t starts = 0;
+    for (uint32_t q = 0; q < 64; ++q) {
+        const uint32_t r = regs[base + q];
+        if (r != p) starts |= 1ULL << q;
+        p = r;
+    }
+    uint32_t *s_first = L.idx;
+    s_first[t] = starts ? base + (uint32_t)__builtin_ctzll(starts) : 16384u;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {  // suffix minimum, in place
+        const uint32_t o = t + off < 256 ? s_first[t + off] : 16384u;
+        __syncthreads();
+        s_first[t] = min(s_first[t], o);
+        __syncthreads();
+    }
+    const uint32_t next_after = t + 1 < 256 ? s_first[t + 1] : 16384u;
+    uint32_t pos, nbytes = 0;
+    const uint32_t nops = sp::block_scan(L, (uint32_t)__builtin_popcountll(starts), pos);
+    for (uint64_t m = starts; m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint64_t later = m & (m - 1);
+        const uint32_t end = later ? base + (uint32_t)__builtin_ctzll(later) : next_after;
+        const uint32_t len = end - (base + j), v = regs[base + j];
+        const uint32_t op = v ? sp::mkval(v, len) : sp::mkzero(len);
+        ops[pos++] = (uint16_t)op;
+        nbytes += sp::bytes(op);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nbytes += __shfl_down(nbytes, off, 64);
+    if ((t & 63) == 0) L.part[t >> 6] = nbytes;
+    __syncthreads();
+    if (t == 0) {
+        state[1] = nops;
+        state[2] = L.part[0] + L.part[1] + L.part[2] + L.part[3];
+    }
+    __syncthreads();  // part[] reuse
 }
 
 template <int ELEN>
@@ -437,8 +519,21 @@ __device__ void replay_one(sp::Lds &L, const HllReplay &it, const KeysDev &elems
     // (a SET string may already exceed the limit and stay sparse through updates that do not grow
     // it: the length argument holds only for strings that start within the limit)
     const uint64_t len0 = 16u + (it.state[1] ? it.state[2] : 2u);
-    if (must_promote(L, it.final_regs, len0 <= max_bytes ? max_bytes : ~0ULL)) {  // uniform
+    bool canon;
+    if (must_promote(L, it.final_regs, len0 <= max_bytes ? max_bytes : ~0ULL, max_bytes, canon)) {  // uniform
         if (threadIdx.x == 0) it.state[0] = 1u;
+        return;
+    }
+    // Shortcut (r04): from a normalized string, updates whose final registers have no nonzero run
+    // longer than 4 and whose bound B (zero-run bytes + one byte per nonzero register, which no
+    // intermediate string exceeds: B only grows as registers are raised) fits the limit end in the
+    // normalized string of the final registers, whatever their order -- hllSparseSet's merges
+    // always join the runs a split or a raise creates when the result is <= 4 long.  Pinned
+    // against the oracle's element-by-element hllSparseSet on random and adversarial update
+    // sequences (tests/test_oracle.py::test_sparse_normalized_shortcut).  The element-by-element
+    // replay below runs only when a condition fails.
+    if (canon && sparse_normalized(L, it)) {  // uniform
+        sparse_encode_normalized(L, it.final_regs, it.ops, it.state);
         return;
     }
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;

@@ -477,3 +477,45 @@ def test_sparse_set_string_beyond_limit(client, fresh):
     s = h.exportString()
     assert s[4] == 0 and s == ref.string(s[8:16])
     h.delete()
+
+
+def test_sparse_first_batches_many_keys(client, fresh):
+    """The sparse-replay shortcut's regime (hll_kernels.hip replay_one, r04): many fresh HLLs in one
+    multi-key PFADD, the keys staying sparse (1,000 elements each: their final registers have no
+    nonzero run longer than 4, so the string is the normalized encoding), then a second batch into
+    the same (normalized) strings, then a third batch that builds runs of five equal registers on
+    some keys (the shortcut must not apply: the element-by-element replay decides the split).  GET
+    bytes equal the element-by-element restatement for every key after every batch."""
+    rng = np.random.default_rng(67)
+    nk = 600
+    keys = [f"{fresh}-{i}" for i in range(nk)]
+    refs = [O.RedisHll() for _ in keys]
+    runs5 = _count1_elements(range(5000, 5005), rng)  # registers 5000..5004 raised to 1
+
+    def batch(per, extra=None):
+        els = [rng.integers(0, 256, size=(per, 16), dtype=np.uint8) for _ in keys]
+        if extra is not None:  # the run of five on every third key, in descending order
+            for i in range(0, nk, 3):
+                els[i] = np.concatenate([els[i], np.frombuffer(b"".join(extra[::-1]), np.uint8).reshape(-1, 16)])
+        segs = np.zeros(nk + 1, np.uint64)
+        segs[1:] = np.cumsum([len(e) for e in els])
+        replies = hll_add_multi(client, keys, segs, Arena.fixed(np.concatenate(els)))
+        for i in range(nk):
+            assert bool(replies[i]) == bool(refs[i].pfadd(*O.fixed_arena(els[i])))
+
+    def check(tag):
+        sparse = 0
+        for k, r in zip(keys, refs):
+            s = client.getHyperLogLog(k).exportString()
+            assert s == r.string(s[8:16]), (tag, k)
+            sparse += s[4] == 1
+        return sparse
+
+    batch(1000)
+    assert check("first") == nk  # all stay sparse (~2,000 bytes each)
+    batch(150)
+    assert check("second") == nk
+    batch(20, extra=runs5)
+    check("third")
+    for k in keys:
+        client.getHyperLogLog(k).delete()

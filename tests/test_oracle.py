@@ -303,3 +303,56 @@ def test_bitset_vectors_on_oracle(bits, size_bits, card):
     got = [i for i in range(len(s) * 8) if s[i >> 3] & (0x80 >> (i & 7))]
     assert got == sorted(bits)  # MSB-first: bit i is byte i >> 3, mask 0x80 >> (i & 7)
     assert f.contains(*O.arena([key_for_bit(0)])) == (1 if 0 in bits else 0)  # get(0) is false
+
+
+def _normalized_bound(regs):
+    """(no nonzero run longer than 4, B = zero-run bytes + one byte per nonzero register)."""
+    r = np.asarray(regs)
+    edges = np.flatnonzero(np.diff(r.astype(np.int16))) + 1
+    starts = np.concatenate([[0], edges])
+    ends = np.concatenate([edges, [16384]])
+    lens, vals = ends - starts, r[starts]
+    zero = vals == 0
+    b = int(np.where(lens[zero] > 64, 2, 1).sum() + lens[~zero].sum())
+    return bool((lens[~zero] <= 4).all()), b
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_sparse_normalized_shortcut(seed):
+    """The property k_hll_sparse_replay's shortcut rests on (hll_kernels.hip replay_one): starting
+    from a normalized sparse string (== hll_sparse_pack of its registers, every nonzero run <= 4),
+    ANY order of hllSparseSet updates whose final registers have no nonzero run longer than 4 and
+    whose bound B (zero-run bytes + one byte per nonzero register) fits hll-sparse-max-bytes ends,
+    without a promotion, in hll_sparse_pack of the final registers.  Checked against the
+    element-by-element restatement on random windows (clustered registers, few values, repeated
+    raises, both ends of the register space) -- the cases where the order could matter."""
+    rng = np.random.default_rng(1000 + seed)
+    tested = 0
+    for _ in range(1000):
+        W = int(rng.choice([int(rng.integers(2, 13)), int(rng.integers(2, 13)), 40, 400, 16384]))
+        base = int(rng.choice([0, 16384 - W, int(rng.integers(0, 16384 - W + 1))]))
+        maxv = int(rng.choice([1, 2, 3, 32]))
+        regs = np.zeros(16384, np.uint8)
+        nv = int(rng.integers(0, W))
+        if nv and rng.random() < 0.7:
+            regs[rng.integers(base, base + W, size=nv)] = rng.integers(1, maxv + 1, size=nv)
+        ok0, _ = _normalized_bound(regs)
+        if not ok0:
+            continue
+        s0 = O.hll_sparse_pack(regs)
+        ops = np.zeros(20000, np.uint8)
+        ops[:len(s0)] = np.frombuffer(s0, np.uint8)
+        n = len(s0)
+        nu = int(rng.integers(1, 2 * min(W, 400) + 4))
+        ur, uc = rng.integers(base, base + W, size=nu), rng.integers(1, maxv + 1, size=nu)
+        fin = regs.copy()
+        np.maximum.at(fin, ur, uc.astype(np.uint8))
+        ok, b = _normalized_bound(fin)
+        if not ok or 16 + b > 3000:
+            continue
+        for r_, c_ in zip(ur, uc):
+            res, n = _sp_set(ops, n, int(r_), int(c_))
+            assert res != 2, "promotion below the B bound"
+        assert ops[:n].tobytes() == O.hll_sparse_pack(fin)
+        tested += 1
+    assert tested > 500
