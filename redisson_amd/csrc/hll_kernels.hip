@@ -658,6 +658,19 @@ void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllRepl
     }
 }
 
+// recycled pool slots zeroed in one launch (registers + state words), one block per slot
+__global__ __launch_bounds__(256) void k_hll_zero(uint8_t *const *__restrict__ regs, uint32_t *const *__restrict__ state) {
+    u8x16 *r = (u8x16 *)regs[blockIdx.x];
+#pragma unroll
+    for (int i = threadIdx.x; i < kHllRegs / 16; i += 256) r[i] = (u8x16)(0);
+    if (threadIdx.x < 4) state[blockIdx.x][threadIdx.x] = 0u;
+}
+
+void launch_hll_zero(uint8_t *const *d_regs, uint32_t *const *d_state, uint32_t n, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_hll_zero, dim3(n), dim3(256), 0, st, d_regs, d_state);
+}
+
 // ---------------------------------------------------------------------------------
 // register exchange: HLL i <-> buf[i * 16384 ..], one block per HLL, 16 B per lane
 // ---------------------------------------------------------------------------------

@@ -214,9 +214,10 @@ struct rbx_ctx {
         uint8_t *regs;
         uint32_t *state;
         uint16_t *ops;
-        bool zeroed;  // a never-used slot of a chunk zero-filled at its creation
     };
-    std::vector<HllSlot> hll_free;  // (registers, state words, sparse opcodes)
+    std::vector<HllSlot> hll_free;   // zeroed slots (registers, state words, sparse opcodes)
+    std::vector<HllSlot> hll_dirty;  // slots of deleted HLLs, zeroed together when hll_free runs out
+    DevBuf hll_zero_ptrs;            // their pointers for k_hll_zero
     DevBuf hll_checks;                     // k_hll_sparse_replay items (cached by content)
     std::vector<HllReplay> check_cache;
 
@@ -281,7 +282,7 @@ rbx::HllState::~HllState() {
     if (d_regs && owner) {
         {
             std::lock_guard<std::recursive_mutex> g(owner->ks.mu);
-            if (!owner->shut) owner->hll_free.push_back({d_regs, d_promoted, d_slot_ops, false});
+            if (!owner->shut) owner->hll_dirty.push_back({d_regs, d_promoted, d_slot_ops});
             if (d_big_ops && !owner->shut) (void)hipFree(d_big_ops);
         }
         ctx_release(owner);
@@ -303,6 +304,24 @@ static int hll_ops_reserve(HllState *h, uint64_t nops) {
 
 // A fresh zeroed HLL register block; the fill runs on `st` (see SlabPool).
 static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out) {
+    if (c->hll_free.empty() && !c->hll_dirty.empty()) {
+        // the deleted HLLs' slots, zeroed in one launch on the caller's stream (creating 10k HLLs
+        // cost 20k small fills, ~10 ms of enqueueing, when each slot was zeroed on its own)
+        const size_t n = c->hll_dirty.size();
+        std::vector<void *> ptrs(2 * n);
+        for (size_t i = 0; i < n; ++i) {
+            ptrs[i] = c->hll_dirty[i].regs;
+            ptrs[n + i] = c->hll_dirty[i].state;
+        }
+        RBX_TRY(c->hll_zero_ptrs.reserve(ptrs.size() * sizeof(void *)));
+        HIP_TRY(hipMemcpyAsync(c->hll_zero_ptrs.p, ptrs.data(), ptrs.size() * sizeof(void *), hipMemcpyHostToDevice, st));
+        uint8_t *const *d_regs = c->hll_zero_ptrs.as<uint8_t *>();
+        launch_hll_zero(d_regs, (uint32_t *const *)(d_regs + n), (uint32_t)n, st);
+        HIP_TRY(hipGetLastError());
+        // handed out last-deleted first, as before
+        c->hll_free.insert(c->hll_free.end(), c->hll_dirty.begin(), c->hll_dirty.end());
+        c->hll_dirty.clear();
+    }
     if (c->hll_free.empty()) {
         // registers of kHllPerChunk HLLs, then their state words, then their sparse opcode lists
         uint8_t *chunk = nullptr;
@@ -315,7 +334,7 @@ static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out)
         HIP_TRY(hipMemsetAsync(chunk, 0, (kHllBytes + kHllStateWords * 4) * kHllPerChunk, st));
         // hand out in reverse so that successive allocations are ascending
         for (size_t i = kHllPerChunk; i-- > 0;)
-            c->hll_free.push_back({chunk + i * kHllBytes, words + i * kHllStateWords, ops + i * (kHllOpsBytes / 2), true});
+            c->hll_free.push_back({chunk + i * kHllBytes, words + i * kHllStateWords, ops + i * (kHllOpsBytes / 2)});
     }
     auto h = std::make_shared<HllState>();
     const auto slot = c->hll_free.back();
@@ -325,11 +344,8 @@ static int hll_alloc(rbx_ctx *c, hipStream_t st, std::shared_ptr<HllState> *out)
     c->hll_free.pop_back();
     h->owner = c;
     c->refs.fetch_add(1);
-    if (!slot.zeroed) {  // a recycled slot: zero it on the caller's stream
-        HIP_TRY(hipMemsetAsync(h->d_regs, 0, kHllBytes, st));
-        // state 0: not promoted, the createHLLObject sparse string (one XZERO)
-        HIP_TRY(hipMemsetAsync(h->d_promoted, 0, kHllStateWords * 4, st));
-    }
+    // every slot in hll_free is zero: registers 0, state 0 (not promoted, the createHLLObject
+    // sparse string: one XZERO)
     *out = h;
     return RBX_OK;
 }
@@ -861,13 +877,16 @@ int rbx_shutdown(rbx_ctx *c) {
         for (auto *p : c->hll_chunks) (void)hipFree(p);
         c->hll_chunks.clear();
         c->hll_free.clear();
+        c->hll_dirty.clear();
+        c->st_t8_entries = c->st_flag_bytes = 0;
         c->slab.reset();  // bitmaps still held by open handles keep their slab alive
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
                           &c->counters, &c->filt_table, &c->probe_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
-                          &c->slot_offs[0], &c->slot_offs[1]}) {
+                          &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
+                          &c->hll_zero_ptrs}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;

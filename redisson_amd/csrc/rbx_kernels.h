@@ -251,6 +251,8 @@ struct HllReplay {
 // one block per item; items whose HLL is already promoted return at once
 void launch_hll_sparse_replay(const KeysDev &elems, int elen_fast, const HllReplay *items, uint32_t n,
                               uint64_t max_bytes, hipStream_t st);
+// zero n pool slots: 16384 register bytes and 4 state words each (kHllStateWords)
+void launch_hll_zero(uint8_t *const *d_regs, uint32_t *const *d_state, uint32_t n, hipStream_t st);
 // buf[i*16384..] = regs[i] (pack) or regs[i] = max(regs[i], buf[i*16384..]) (unpack_max)
 void launch_hll_pack(uint8_t *const *d_regs, uint32_t n, uint8_t *buf, bool unpack_max, hipStream_t st);
 

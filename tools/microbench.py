@@ -303,6 +303,25 @@ def main():
         import numpy as np
 
         NH = 10_000
+        # warm-up on other keys (module loading, pool chunks), deleted again: the measured keys
+        # then reuse those pool slots (zeroed together on the first allocation)
+        wel = torch.randint(0, 256, (NH * 10, 16), dtype=torch.uint8, device="cuda")
+        wh = []
+        for i in range(NH):
+            hp = C.c_void_p()
+            assert L.lib().rbx_hll_open(client.ctx, f"hw-{i}".encode(), 1, C.byref(hp)) == 0
+            wh.append(hp.value)
+        warr = (C.c_void_p * NH)(*wh)
+        wseg = np.arange(NH + 1, dtype=np.uint64) * np.uint64(10)
+        wch = torch.zeros(NH, dtype=torch.int32, device="cuda")
+        wdk = device_keys(wel.data_ptr(), NH * 10, 16)
+        assert L.lib().rbx_hll_add_multi_dev(client.ctx, warr, NH, None, wseg.ctypes.data_as(L.u64p), C.byref(wdk),
+                                             wch.data_ptr(), sp) == 0
+        torch.cuda.synchronize()
+        for hp in wh:
+            L.lib().rbx_hll_close(C.c_void_p(hp))
+        for i in range(NH):
+            client.getHyperLogLog(f"hw-{i}").delete()
         for per in (1_000, 10_000):
             hs = []
             for i in range(NH):

@@ -17,7 +17,7 @@ RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9" \
 fi
 [[ ",$ONLY," == *",c4,"* ]] && { timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c4" --workload c4 || exit 1 ; }
 if [[ ",$ONLY," == *",c5,"* ]]; then
-RBX_STREAM_BYTES="k_stream_contains_q=3.84e8 k_stream_contains=3.84e8 k_stream_probe=4.27e7 k_stream_commit=4.27e7" \
+RBX_STREAM_BYTES="k_stream_contains_q=3.84e8 k_stream_contains=3.84e8 k_stream_probe=4.27e7 k_stream_probe8=4.27e7 k_stream_commit=4.27e7" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c5" --workload c5 || exit 1
 fi
 python3 - "$R/gpurun_out" "$TAG" <<'PY'
