@@ -519,3 +519,37 @@ def test_sparse_first_batches_many_keys(client, fresh):
     check("third")
     for k in keys:
         client.getHyperLogLog(k).delete()
+
+
+def test_sparse_set_string_past_the_slot_copies(client, fresh):
+    """a pool slot's opcode list holds 3,072 opcodes (a PFADD-built string never exceeds
+    the 3,000-byte limit); a SET string with more (here 6,001 opcodes) moves to its own list.  It
+    survives a device-to-device copy to another context (rbx_hll_copy_to, the node's cross-GPU
+    PFCOUNT / PFMERGE input) byte for byte, and the copy keeps replaying like the original."""
+    import ctypes as C
+
+    from redisson_amd import RedissonClient
+    from redisson_amd import _lib as L
+
+    rng = np.random.default_rng(68)
+    ops = bytearray()
+    for _ in range(3000):
+        ops += bytes([0x80, 0x00])
+    rest = 16384 - 6000
+    ops += bytes([0x40 | ((rest - 1) >> 8), (rest - 1) & 0xFF])
+    s0 = _header(1, bytes(7) + b"\x80") + bytes(ops)
+    client.getHyperLogLog(fresh).importString(s0)
+    with RedissonClient(0) as other:
+        src, keep1 = L.name_struct(fresh)
+        dst, keep2 = L.name_struct(fresh + "-copy")
+        assert L.lib().rbx_hll_copy_to(client.ctx, src, other.ctx, dst) == 0
+        g = other.getHyperLogLog(fresh + "-copy")
+        assert g.exportString() == s0
+        raise2 = _count_elements(range(0, 40, 2), 2, rng)  # in place: no growth, stays sparse
+        g.addAll(Arena(raise2))
+        ref = O.RedisHll.from_string(s0)
+        ref.pfadd(*O.arena(raise2))
+        s = g.exportString()
+        assert s[4] == 1 and s == ref.string(s[8:16])
+        g.delete()
+    client.getHyperLogLog(fresh).delete()
