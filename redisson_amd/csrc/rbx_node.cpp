@@ -10,8 +10,10 @@
 // uploads and kernels of different GPUs overlap) and gathered back in segment order.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -42,8 +44,64 @@ using HandleRef = std::shared_ptr<NodeHandle>;
 // long-lived node with tenant churn does not keep one handle per name it ever served.
 constexpr size_t kMaxCachedHandles = 1u << 20;
 
+// One worker thread per GPU of the node: a call's per-GPU parts run on the GPUs' workers
+// concurrently (r03 started a std::thread per GPU per call).  Worker g runs GPU g's parts in the
+// order they are submitted.
+class GpuWorkers {
+  public:
+    explicit GpuWorkers(int n) : ws_(n) {
+        for (auto &w : ws_) {
+            w = std::make_unique<W>();
+            W *p = w.get();
+            p->th = std::thread([p] { p->loop(); });
+        }
+    }
+    ~GpuWorkers() {
+        for (auto &w : ws_) {
+            {
+                std::lock_guard<std::mutex> lk(w->mu);
+                w->stop = true;
+            }
+            w->cv.notify_one();
+            w->th.join();
+        }
+    }
+    void submit(int g, std::function<void()> f) {
+        W &w = *ws_[g];
+        {
+            std::lock_guard<std::mutex> lk(w.mu);
+            w.q.push_back(std::move(f));
+        }
+        w.cv.notify_one();
+    }
+
+  private:
+    struct W {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<std::function<void()>> q;
+        bool stop = false;
+        void loop() {
+            for (;;) {
+                std::function<void()> f;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || !q.empty(); });
+                    if (q.empty()) return;  // stop, and nothing left
+                    f = std::move(q.front());
+                    q.pop_front();
+                }
+                f();
+            }
+        }
+    };
+    std::vector<std::unique_ptr<W>> ws_;
+};
+
 struct rbx_node {
     std::vector<rbx_ctx *> ctx;
+    std::unique_ptr<GpuWorkers> workers;
     std::mutex mu;                                           // the handle cache and the replica set
     std::map<std::pair<int, std::string>, HandleRef> blooms;  // open handles per (GPU, name)
     // Bloom filters replicated on every GPU (rbx_node_bloom_replicate): adds go to every replica,
@@ -84,10 +142,10 @@ static int check_name(const rbx_name &n) {
         if (r_ != RBX_OK) return r_;   \
     } while (0)
 
-// Runs fn(g) for every GPU g with work, concurrently when more than one; the first failure (in
-// GPU order) becomes this thread's error.
+// Runs fn(g) for every GPU g with work, concurrently (on the GPUs' workers) when more than one;
+// the first failure (in GPU order) becomes this thread's error.  fn must not call per_gpu.
 template <class Fn>
-static int per_gpu(const std::vector<int> &gpus, Fn &&fn) {
+static int per_gpu(rbx_node *nd, const std::vector<int> &gpus, Fn &&fn) {
     struct Res {
         int rc = RBX_OK;
         std::string msg;
@@ -95,14 +153,22 @@ static int per_gpu(const std::vector<int> &gpus, Fn &&fn) {
     std::vector<Res> res(gpus.size());
     auto run = [&](size_t i) {
         res[i].rc = fn(gpus[i]);
-        if (res[i].rc != RBX_OK) res[i].msg = rbx_last_error();
+        if (res[i].rc != RBX_OK) res[i].msg = rbx_last_error();  // the worker's thread-local message
     };
     if (gpus.size() == 1) {
         run(0);
     } else {
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < gpus.size(); ++i) th.emplace_back(run, i);
-        for (auto &t : th) t.join();
+        std::mutex mu;
+        std::condition_variable cv;
+        size_t left = gpus.size();
+        for (size_t i = 0; i < gpus.size(); ++i)
+            nd->workers->submit(gpus[i], [&, i] {
+                run(i);
+                std::lock_guard<std::mutex> lk(mu);
+                if (--left == 0) cv.notify_one();
+            });
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left == 0; });
     }
     for (auto &r : res)
         if (r.rc != RBX_OK) return fail(r.rc, r.msg);
@@ -131,6 +197,7 @@ int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
         }
         nd->ctx.push_back(c);
     }
+    nd->workers = std::make_unique<GpuWorkers>(n_gpus);
     *out = nd;
     return RBX_OK;
 }
@@ -138,6 +205,7 @@ int rbx_node_init(int n_gpus, const int *devices, rbx_node **out) {
 int rbx_node_shutdown(rbx_node *nd) {
     if (!nd) return RBX_OK;
     nd->blooms.clear();  // closes every cached handle (no batch may run during shutdown)
+    nd->workers.reset();  // idle: joined
     int rc = RBX_OK;
     for (rbx_ctx *c : nd->ctx) {
         const int r = rbx_shutdown(c);
@@ -255,7 +323,7 @@ int rbx_node_bloom_add(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, c
         std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
         if (!is_replicated(nd, nm) || nd->ctx.size() == 1)
             return node_add_on(nd, home, name, size, k, keys, out_new, out_count);
-        rc = per_gpu(all_gpus(nd), [&](int g) -> int {
+        rc = per_gpu(nd, all_gpus(nd), [&](int g) -> int {
             uint64_t cnt = 0;
             return node_add_on(nd, g, name, size, k, keys, g == home ? out_new : nullptr,
                                g == home ? out_count : &cnt);
@@ -283,7 +351,7 @@ int rbx_node_bloom_contains(rbx_node *nd, rbx_name name, uint64_t size, uint32_t
         return rbx_bloom_contains_n(nd->ctx[home], name, size, k, keys, out_present, out_count);
     if (keys->n && !keys->bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
     std::vector<uint64_t> cnt(N, 0);
-    NODE_TRY(per_gpu(all_gpus(nd), [&](int g) -> int {
+    NODE_TRY(per_gpu(nd, all_gpus(nd), [&](int g) -> int {
         const uint64_t i0 = keys->n * (uint64_t)g / N, i1 = keys->n * (uint64_t)(g + 1) / N;
         rbx_keys sub = keys->offsets ? rbx_keys{keys->bytes, keys->offsets + i0, 0, i1 - i0}
                                      : rbx_keys{keys->bytes + i0 * keys->stride, nullptr, keys->stride, i1 - i0};
@@ -315,7 +383,7 @@ int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
     if (on) {
         rbx_bloom_config cfg;
         NODE_TRY(rbx_bloom_read_config_n(nd->ctx[home], name, &cfg));  // not initialized: ISE
-        const int rc = per_gpu(others, [&](int g) -> int { return rbx_bloom_copy_to(nd->ctx[home], nd->ctx[g], name); });
+        const int rc = per_gpu(nd, others, [&](int g) -> int { return rbx_bloom_copy_to(nd->ctx[home], nd->ctx[g], name); });
         if (rc != RBX_OK) {  // a partial copy (or re-sync) is not a replica: drop whatever landed
             const std::string msg = rbx_last_error();
             {
@@ -346,7 +414,7 @@ int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
         }
     }
     evicted.clear();
-    return per_gpu(others, [&](int g) -> int {
+    return per_gpu(nd, others, [&](int g) -> int {
         int d;
         return rbx_del_n(nd->ctx[g], both, 2, &d);
     });
@@ -575,7 +643,7 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
         }
         build_parts(nd, sn, seg, keys, &parts, &repl, is_add);
         gpus = gpus_with_work(parts);
-        rc = per_gpu(gpus, [&](int g) -> int {
+        rc = per_gpu(nd, gpus, [&](int g) -> int {
             Part &p = parts[g];
             if (is_add && injected_add_fault(nd, g)) return fail(RBX_E_DEVICE, "injected add fault (rbx_node_test_fail_adds)");
             for (int attempt = 0;; ++attempt) {
@@ -637,7 +705,7 @@ int rbx_node_hll_add_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, c
     std::vector<Part> parts;
     build_parts(nd, sn, seg_offsets, elements, &parts);
     const std::vector<int> gpus = gpus_with_work(parts);
-    const int rc = per_gpu(gpus, [&](int g) -> int {
+    const int rc = per_gpu(nd, gpus, [&](int g) -> int {
         Part &p = parts[g];
         std::vector<rbx_name> nm(p.segs.size());
         for (size_t j = 0; j < p.segs.size(); ++j) nm[j] = name_ref(sn[p.segs[j]]);
