@@ -141,3 +141,44 @@ def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, prefilter):
     wc = _c5_case(client, fresh, seed=0xC5100 + prefilter, nt=100_000, expected=1000, fpp=1e-3, n=2_100_000,
                   chunk=700_000, prefilter=prefilter)
     assert wc[1] > 10_000
+
+
+@pytest.mark.parametrize("table8", [1, 0])
+def test_stream_k20_variable_keys(client, fresh, table8):
+    """The stream's KMAX = 32 instantiation and variable-length keys (KLEN = 0: the generic hash
+    path of the probe, both contains kernels and the 8-byte table): tryInit(10_000, 1e-6) tenants
+    (k = 20), keys of 0..90 bytes, adds and contains of the same keys interleaved, 3 chunks."""
+    rng = np.random.default_rng(0xC520 + table8)
+    from redisson_amd import Arena
+
+    nt = 40
+    names = [f"{fresh}-{t}" for t in range(nt)]
+    refs, handles = [], []
+    for nm in names:
+        f = client.getBloomFilter(nm)
+        assert f.tryInit(10_000, 1e-6)
+        refs.append(O.OracleBloom(f.getSize(), f.getHashIterations()))
+        handles.append(BloomHandle(client, nm))
+    assert refs[0].k == 20
+    n = 60_000
+    pool = [rng.bytes(int(x)) for x in rng.integers(0, 91, size=n // 3)]
+    keys = [pool[int(i)] for i in rng.integers(0, len(pool), size=n)]
+    kf = _zipf_tenants(rng, nt, n)
+    op = (rng.random(n) < 0.3).astype(np.uint8)
+    assert L.lib().rbx_tune(b"stream_chunk", 20_000) == 0
+    assert L.lib().rbx_tune(b"stream_table8", table8) == 0
+    try:
+        out, counts = bloom_stream(client, handles, kf, op, Arena(keys))
+    finally:
+        L.lib().rbx_tune(b"stream_chunk", 0)
+        L.lib().rbx_tune(b"stream_table8", 1)
+    buf, offs = O.arena(keys)
+    want, wc = O.bloom_stream(refs, kf, op, buf, offs)
+    assert np.array_equal(out, want) and [int(counts[0]), int(counts[1])] == wc
+    assert wc[0] > 0 and wc[1] > 0
+    for nm, r in zip(names, refs):
+        assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
+    for h in handles:
+        h.close()
+    for nm in names:
+        client.getBloomFilter(nm).delete()
