@@ -283,8 +283,8 @@ rbx::HllState::~HllState() {
         {
             std::lock_guard<std::recursive_mutex> g(owner->ks.mu);
             if (!owner->shut) owner->hll_dirty.push_back({d_regs, d_promoted, d_slot_ops});
-            if (d_big_ops && !owner->shut) (void)hipFree(d_big_ops);
         }
+        if (d_big_ops) (void)hipFree(d_big_ops);  // its own allocation: released also after a shutdown
         ctx_release(owner);
     }
 }
