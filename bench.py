@@ -291,9 +291,13 @@ def request_fields(traffic_json, kernel, ms, peak, write_peak=None):
     reqs = load_traffic(traffic_json, kernel, "requests_per_launch")
     rd = load_traffic(traffic_json, kernel, "read_requests_per_launch")
     wr = load_traffic(traffic_json, kernel, "write_requests_per_launch")
+    at = load_traffic(traffic_json, kernel, "atomic_requests_per_launch")
     out = {"requests_per_launch": reqs, "request_rate_per_s": reqs / (ms / 1e3) if reqs else None,
            "request_peak_per_s": peak, "read_requests_per_launch": rd, "write_requests_per_launch": wr,
-           "write_request_peak_per_s": write_peak}
+           "write_request_peak_per_s": write_peak,
+           # atomic requests (PMC TCC_ATOMIC; all of them execute at the memory side and are
+           # counted in the write requests too) and their throughput at this call time
+           "atomic_requests_per_launch": at, "atomic_rate_per_s": at / (ms / 1e3) if at else None}
     if rd is not None and wr is not None and peak and write_peak:
         floor_s = rd / peak + wr / write_peak
         out["request_floor_ms"] = floor_s * 1e3
@@ -575,6 +579,9 @@ def run_c2(args, world, rank, local):
                                   load_traffic(args.traffic_json, "add_pipeline")) if pmc_ok else None,
                   "add_requests_per_call": load_traffic(args.traffic_json, "add_pipeline", "requests_per_launch")
                   if pmc_ok else None,
+                  # of which atomics (PMC TCC_ATOMIC: non-owner counters, stage-1 reservations)
+                  "add_atomic_requests_per_call": load_traffic(args.traffic_json, "add_pipeline",
+                                                               "atomic_requests_per_launch") if pmc_ok else None,
                   "host_path": hostpath,
                   "c2_tryinit_nonpow2": nonpow2},
     }
