@@ -46,13 +46,16 @@ enum {
     RBX_E_OOM = -7,              /* device or host allocation failure                */
     RBX_E_NO_SUCH_KEY = -8,      /* RedisException "ERR no such key" (RENAME)        */
     RBX_E_REDIS = -9,            /* other RedisException replies, e.g. "ERR bit offset is not an
-                                    integer or out of range" (a negative-size filter past 2^32 bits).
-                                    Intended divergence: the engine refuses every open / add /
-                                    contains of a filter with |size| > 2^32 up front, while Redis
-                                    fails a batch only when one of its indexes (hash % size) is
-                                    >= 2^32 -- for |size| just above 2^32 most reference batches
-                                    succeed.  Such sizes come only from tryInit with a negative
-                                    expectedInsertions (M/RedissonBloomFilter.java:262-277). */
+                                    integer or out of range": a filter with |size| > 2^32 (only from
+                                    tryInit with a negative expectedInsertions,
+                                    M/RedissonBloomFilter.java:262-277) whose batch reaches an index
+                                    (hash % |size|) past the Redis offset limit 2^32 - 1.  As in the
+                                    reference's pipelined batch, rbx_bloom_add[_n] has then set every
+                                    in-range bit (and created the key only if one was set) and
+                                    rbx_bloom_contains[_n] changed nothing; a batch with no such
+                                    index gets the exact in-order replies.  Handles (rbx_bloom_open*,
+                                    hence the *_dev / multi-tenant / stream calls) and replica
+                                    copies of such a filter are refused up front with this code. */
     RBX_E_TIMEOUT = -10          /* rbx_future_wait: the call has not completed in time        */
 };
 

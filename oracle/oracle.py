@@ -174,7 +174,8 @@ class OracleBloom:
 
     def __init__(self, size: int, k: int):
         self.size, self.k = int(size), int(k)  # size: the Java long (negative sizes index [0, |size|))
-        self.bitmap = np.zeros((abs(self.size) + 7) // 8 + 1, dtype=np.uint8)
+        # a Redis string holds at most 2^32 bits (offsets past it are errors: orc_bloom_add)
+        self.bitmap = np.zeros((min(abs(self.size), 1 << 32) + 7) // 8 + 1, dtype=np.uint8)
         self.redis_len = 0
 
     def add(self, buf, offs, per_key: bool = False):

@@ -108,9 +108,10 @@ def highway_hash128(data: bytes, key=REDISSON_KEY) -> tuple[int, int]:
 
 
 def bloom_indexes(h1: int, h2: int, k: int, size: int) -> list[int]:
+    # Java's `x % size` takes the dividend's sign: for x >= 0 it is x % |size| (negative sizes too)
     out, h = [], h1
     for i in range(k):
-        out.append((h & 0x7FFFFFFFFFFFFFFF) % size)
+        out.append((h & 0x7FFFFFFFFFFFFFFF) % abs(size))
         h = (h + (h2 if i % 2 == 0 else h1)) & M64
     return out
 

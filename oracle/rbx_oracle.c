@@ -272,46 +272,71 @@ static int setbit(uint8_t *bm, uint64_t *redis_len, uint64_t i) {
     return old;
 }
 
+/* Redis bit offsets end at 2^32 - 1 [redis-7.2 bitops.c getBitOffsetFromArgument: 512 MiB strings]:
+ * SETBIT / GETBIT past it reply "ERR bit offset is not an integer or out of range" without touching
+ * the key.  Only a filter whose |size| exceeds 2^32 (tryInit with a negative expectedInsertions,
+ * M/RedissonBloomFilter.java:262-277) produces such indexes.  In a pipelined batch every other
+ * command still runs, and the batch then fails (CommandBatchService: the first error reply
+ * completes execute() exceptionally) -- so add() has set every in-range bit and throws. */
+#define ORC_MAX_OFFSET 0xFFFFFFFFULL
+#define ORC_E_REDIS (-9)
+
 /* add(Collection) :104-137: n*k SETBITs executed in submission order
  * (CommandBatchService ordering), then the fold over windows of s = k replies.
- * Returns the count, or -4 (ArithmeticException "/ by zero") for n == 0. */
+ * Returns the count, -4 (ArithmeticException "/ by zero") for n == 0, or -9 (RedisException: an
+ * index past the Redis offset limit; every in-range bit is set). */
 int64_t orc_bloom_add(uint8_t *bitmap, uint64_t *redis_len, const uint8_t *bytes,
                       const uint64_t *offsets, uint64_t n, int k, int64_t size, uint8_t *out_new) {
     if (n == 0) return -4;
     int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)k);
     int64_t c = 0;
+    int err = 0;
     for (uint64_t i = 0; i < n; i++) {
         uint64_t h[2];
         orc_redisson_hash128(bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), h);
         orc_bloom_indexes(h[0], h[1], k, size, idx);
         int zeros = 0;
-        for (int j = 0; j < k; j++)
+        for (int j = 0; j < k; j++) {
+            if ((uint64_t)idx[j] > ORC_MAX_OFFSET) {
+                err = 1;
+                continue;
+            }
             if (!setbit(bitmap, redis_len, (uint64_t)idx[j])) zeros++;
+        }
         if (out_new) out_new[i] = zeros > 0;
         if (zeros > 0) c++;
     }
     free(idx);
+    if (err) return ORC_E_REDIS;
     return (int64_t)(int32_t)c; /* `int c` accumulator in Java */
 }
 
-/* contains(Collection) :153-186: objects.size() - missed.  -4 for n == 0. */
+/* contains(Collection) :153-186: objects.size() - missed.  -4 for n == 0, -9 (RedisException) when
+ * an index is past the Redis offset limit (GETBIT replies an error; nothing is changed). */
 int64_t orc_bloom_contains(const uint8_t *bitmap, uint64_t redis_len, const uint8_t *bytes,
                            const uint64_t *offsets, uint64_t n, int k, int64_t size,
                            uint8_t *out_present) {
     if (n == 0) return -4;
     int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)k);
     int64_t missed = 0;
+    int err = 0;
     for (uint64_t i = 0; i < n; i++) {
         uint64_t h[2];
         orc_redisson_hash128(bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), h);
         orc_bloom_indexes(h[0], h[1], k, size, idx);
         int zeros = 0;
-        for (int j = 0; j < k; j++)
+        for (int j = 0; j < k; j++) {
+            if ((uint64_t)idx[j] > ORC_MAX_OFFSET) {
+                err = 1;
+                continue;
+            }
             if (!getbit(bitmap, redis_len, (uint64_t)idx[j])) zeros++;
+        }
         if (out_present) out_present[i] = zeros == 0;
         if (zeros > 0) missed++;
     }
     free(idx);
+    if (err) return ORC_E_REDIS;
     return (int64_t)n - missed;
 }
 

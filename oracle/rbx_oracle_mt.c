@@ -22,6 +22,13 @@
 
 void orc_redisson_hash128(const uint8_t *data, size_t len, uint64_t out[2]);
 void orc_bloom_indexes(uint64_t hash1, uint64_t hash2, int iterations, int64_t size, int64_t *out);
+int64_t orc_bloom_add(uint8_t *bitmap, uint64_t *redis_len, const uint8_t *bytes, const uint64_t *offsets,
+                      uint64_t n, int k, int64_t size, uint8_t *out_new);
+int64_t orc_bloom_contains(const uint8_t *bitmap, uint64_t redis_len, const uint8_t *bytes,
+                           const uint64_t *offsets, uint64_t n, int k, int64_t size, uint8_t *out_present);
+
+/* |size| past 2^32 bits: the single-thread functions (the Redis offset limit, rbx_oracle.c) */
+static int wide_size(int64_t size) { return (size < 0 ? 0 - (uint64_t)size : (uint64_t)size) > (1ULL << 32); }
 
 typedef struct {
     const uint8_t *bitmap;
@@ -68,6 +75,7 @@ int64_t orc_bloom_contains_mt(const uint8_t *bitmap, uint64_t redis_len, const u
                               int nthreads) {
     if (n == 0) return -4;
     if (k > 64) return -1;
+    if (wide_size(size)) return orc_bloom_contains(bitmap, redis_len, bytes, offsets, n, k, size, out_present);
     if (nthreads < 1) nthreads = 1;
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     orc_job *jobs = (orc_job *)calloc((size_t)nthreads, sizeof(orc_job));
@@ -127,6 +135,7 @@ static void *setbit_worker(void *p) {
 int64_t orc_bloom_add_mt(uint8_t *bitmap, uint64_t *redis_len, const uint8_t *bytes, const uint64_t *offsets,
                          uint64_t n, int k, int64_t size, uint8_t *out_new, int nthreads) {
     if (n == 0) return -4;
+    if (wide_size(size)) return orc_bloom_add(bitmap, redis_len, bytes, offsets, n, k, size, out_new);
     if (nthreads < 1) nthreads = 1;
     memset(out_new, 0, (size_t)n);
     const uint64_t m = size < 0 ? 0 - (uint64_t)size : (uint64_t)size;

@@ -1685,4 +1685,122 @@ void launch_gather_regions(const uint32_t *tbl, uint64_t nwords, uint64_t region
     hipLaunchKernelGGL(k_gather_regions, dim3(grid), dim3(256), 0, st, tbl, nregions, region_words,
                        total_lanes / nregions, sink);
 }
+
+// ---------------------------------------------------------------------------------
+// Filters past the Redis offset limit: |size| > 2^32, reachable only through tryInit with a
+// negative expectedInsertions (M/RedissonBloomFilter.java:262-277).  The reference's indexes are
+// (h & Long.MAX_VALUE) % size in 64 bits (:139-151); a SETBIT / GETBIT at an offset past 2^32 - 1
+// is an error reply that leaves the key alone while the batch's other commands still run, and the
+// batch then throws (include/rbx.h RBX_E_REDIS).  A correctness path, not a hot one: plain 64-bit
+// remainders, and a first-setter hash table (min key per initially-zero bit) for the in-order add
+// replies -- a key is new iff it is the first setter of one of its bits.
+// ---------------------------------------------------------------------------------
+constexpr unsigned long long kWideEmpty = ~0ULL;
+constexpr uint64_t kMaxOffset = 0xFFFFFFFFULL;
+
+__device__ __forceinline__ uint32_t wide_slot(uint64_t idx, uint32_t tlog2) {
+    return (uint32_t)((idx * 0x9E3779B97F4A7C15ULL) >> (64 - tlog2));
+}
+
+// add pass 1: every in-range bit that is 0 before the chunk gets its smallest key (entry = bit << 32 | key)
+__global__ __launch_bounds__(256) void k_wide_claim(KeysDev keys, uint64_t m, uint32_t k, const uint32_t *__restrict__ bm,
+                                                    unsigned long long *__restrict__ T, uint32_t tlog2) {
+    const uint32_t mask = (1u << tlog2) - 1u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < keys.n; i += (uint64_t)gridDim.x * 256) {
+        uint64_t h1, h2;
+        hash_key<0>(keys, i, h1, h2);
+        uint64_t h = h1;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t idx = (h & 0x7fffffffffffffffULL) % m;
+            h += (j & 1) ? h1 : h2;
+            if (idx > kMaxOffset || (bm[idx >> 5] & bit_in_word((uint32_t)idx))) continue;
+            const unsigned long long e = (unsigned long long)idx << 32 | i;
+            for (uint32_t s = wide_slot(idx, tlog2);; s = (s + 1u) & mask) {
+                const unsigned long long prev = atomicCAS(&T[s], kWideEmpty, e);
+                if (prev == kWideEmpty) break;
+                if ((prev >> 32) == idx) {  // same bit: the smaller key wins (equal high halves)
+                    atomicMin(&T[s], e);
+                    break;
+                }
+            }
+        }
+    }
+}
+
+// add pass 2: replies, the first setters' SETBITs (and the Redis string length), the error flag
+__global__ __launch_bounds__(256) void k_wide_resolve(KeysDev keys, uint64_t m, uint32_t k, uint32_t *__restrict__ bm,
+                                                      unsigned long long *__restrict__ len,
+                                                      const unsigned long long *__restrict__ T, uint32_t tlog2,
+                                                      uint8_t *__restrict__ out, unsigned long long *__restrict__ count,
+                                                      unsigned long long *__restrict__ oob) {
+    const uint32_t mask = (1u << tlog2) - 1u;
+    uint64_t added = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < keys.n; i += (uint64_t)gridDim.x * 256) {
+        uint64_t h1, h2;
+        hash_key<0>(keys, i, h1, h2);
+        uint64_t h = h1;
+        bool fresh = false, bad = false;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t idx = (h & 0x7fffffffffffffffULL) % m;
+            h += (j & 1) ? h1 : h2;
+            if (idx > kMaxOffset) {
+                bad = true;
+                continue;
+            }
+            for (uint32_t s = wide_slot(idx, tlog2);; s = (s + 1u) & mask) {
+                const unsigned long long e = T[s];
+                if (e == kWideEmpty) break;  // the bit was already 1
+                if ((e >> 32) == idx) {
+                    if ((uint32_t)e == (uint32_t)i) {  // this key's SETBIT is the one that replied 0
+                        fresh = true;
+                        atomicOr(&bm[idx >> 5], bit_in_word((uint32_t)idx));
+                        raise_redis_len(len, (idx >> 3) + 1);
+                    }
+                    break;
+                }
+            }
+        }
+        if (out) out[i] = fresh;
+        added += fresh;
+        if (bad) *oob = 1;
+    }
+    block_add_u64(added, count);
+}
+
+// contains: every in-range bit set; an index past the limit flags the call (GETBIT's error reply)
+__global__ __launch_bounds__(256) void k_wide_contains(KeysDev keys, uint64_t m, uint32_t k,
+                                                       const uint32_t *__restrict__ bm, uint8_t *__restrict__ out,
+                                                       unsigned long long *__restrict__ count,
+                                                       unsigned long long *__restrict__ oob) {
+    uint64_t present = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < keys.n; i += (uint64_t)gridDim.x * 256) {
+        uint64_t h1, h2;
+        hash_key<0>(keys, i, h1, h2);
+        uint64_t h = h1;
+        bool all = true, bad = false;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t idx = (h & 0x7fffffffffffffffULL) % m;
+            h += (j & 1) ? h1 : h2;
+            if (idx > kMaxOffset) bad = true;
+            else if (!bm || !(bm[idx >> 5] & bit_in_word((uint32_t)idx))) all = false;  // no key: GETBIT reads 0
+        }
+        if (out) out[i] = all;
+        present += all;
+        if (bad) *oob = 1;
+    }
+    block_add_u64(present, count);
+}
+
+void launch_bloom_wide(const KeysDev &keys, uint64_t m, uint32_t k, uint32_t *bm, unsigned long long *len,
+                       unsigned long long *table, uint32_t tlog2, bool is_add, uint8_t *out,
+                       unsigned long long *count, unsigned long long *oob, hipStream_t st) {
+    const unsigned grid = grid_for(keys.n, kMaxGrid);
+    if (!is_add) {
+        hipLaunchKernelGGL(k_wide_contains, dim3(grid), dim3(256), 0, st, keys, m, k, bm, out, count, oob);
+        return;
+    }
+    hipLaunchKernelGGL(k_wide_claim, dim3(grid), dim3(256), 0, st, keys, m, k, bm, table, tlog2);
+    hipLaunchKernelGGL(k_wide_resolve, dim3(grid), dim3(256), 0, st, keys, m, k, bm, len, table, tlog2, out, count,
+                       oob);
+}
 }  // namespace rbx

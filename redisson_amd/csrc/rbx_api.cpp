@@ -196,6 +196,7 @@ struct rbx_ctx {
     // missing key reads 0; the key is not created), grown on demand, never written by a kernel
     DevBuf zero_bm;
     DevBuf hll_pack;                                // contiguous registers for the RCCL merge
+    DevBuf wide_table;  // first-setter table of |size| > 2^32 adds (bloom_wide_op)
     std::vector<HllSeg> tile_cache;  // content of hll_tiles (valid when tiles_valid)
     bool tiles_valid = false;
     std::vector<FilterDesc> filt_cache;  // content of filt_table
@@ -886,7 +887,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs}) {
+                          &c->hll_zero_ptrs, &c->wide_table}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -1037,6 +1038,51 @@ static int pipelined_host_batches(rbx_ctx *c, const rbx_keys *k, hipStream_t st,
 }
 extern "C" {
 
+// add / contains of a filter whose |size| exceeds 2^32 bits (tryInit with a negative
+// expectedInsertions, M/RedissonBloomFilter.java:262-277), with the reference's semantics: indexes
+// are taken mod |size| in 64 bits; a SETBIT / GETBIT past the Redis offset limit is an error reply
+// that leaves the key alone while every other command of the batch runs; the call then fails with
+// RBX_E_REDIS (RedisException) -- an add has set every in-range bit.  Without such an index the
+// replies are the in-order ones.  Chunks run in key order (each sees the previous chunks' bits).
+static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t k, Bitmap *bm, uint8_t *out_flags,
+                         uint64_t *out_count, bool is_add) {
+    RBX_TRY(c->counters.reserve(64));
+    auto *d_count = c->counters.as<unsigned long long>();
+    auto *d_oob = d_count + 4;
+    HIP_TRY(hipMemsetAsync(d_count, 0, 8, c->stream));
+    HIP_TRY(hipMemsetAsync(d_oob, 0, 8, c->stream));
+    uint8_t *d_out = nullptr;
+    if (out_flags) {
+        RBX_TRY(c->out_bytes.reserve(keys->n));
+        d_out = c->out_bytes.as<uint8_t>();
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    RBX_TRY(pipelined_host_batches(c, keys, c->stream, [&](const KeysDev &dk, uint64_t i0) -> int {
+        if (dk.n >= (1ULL << 32)) return fail(RBX_E_ILLEGAL_ARGUMENT, "chunk exceeds 2^32 keys");
+        uint32_t tl = 10;  // table >= 2x the chunk's bit indexes
+        while ((1ULL << tl) < 2 * dk.n * k) ++tl;
+        unsigned long long *table = nullptr;
+        if (is_add) {
+            RBX_TRY(c->wide_table.reserve(8ULL << tl));
+            table = c->wide_table.as<unsigned long long>();
+            HIP_TRY(hipMemsetAsync(table, 0xff, 8ULL << tl, c->stream));
+        }
+        launch_bloom_wide(dk, m, k, bm ? bm->d_words : nullptr, bm ? bm->d_len : nullptr, table, tl, is_add,
+                          d_out ? d_out + i0 : nullptr, d_count, d_oob, c->stream);
+        HIP_TRY(hipGetLastError());
+        return RBX_OK;
+    }));
+    int rc;
+    const uint64_t oob = read_dev_u64(c, d_oob, &rc);
+    RBX_TRY(rc);
+    if (oob) return fail(RBX_E_REDIS, "ERR bit offset is not an integer or out of range");
+    if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
+    const uint64_t cnt = read_dev_u64(c, d_count, &rc);
+    RBX_TRY(rc);
+    if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
+    return RBX_OK;
+}
+
 static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint32_t k, const rbx_keys *keys,
                          uint8_t *out_flags, uint64_t *out_count, bool is_add) {
     RBX_TRY(validate_keys(keys));
@@ -1052,8 +1098,18 @@ static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint
     }
     RBX_TRY(ks_config_check(c->ks, name, size, k));
     if (keys->n == 0) return fail(RBX_E_ARITHMETIC, "/ by zero");
-    RBX_TRY(check_offsets(size));
     std::shared_ptr<Bitmap> bm;
+    if (size_bits(size) > kEngineMaxSize) {  // indexes may pass the Redis offset limit (bloom_wide_op)
+        const bool existed = c->ks.find(name) != nullptr;
+        RBX_TRY(bitmap_for(c, name, kEngineMaxSize, is_add, c->stream, &bm));
+        const int rc = bloom_wide_op(c, keys, size_bits(size), k, bm.get(), out_flags, out_count, is_add);
+        if (bm && !existed) {  // only valid SETBITs create the key: a batch of error replies leaves none
+            int r2;
+            const uint64_t len = read_dev_u64(c, bm->d_len, &r2);
+            if (r2 == RBX_OK && len == 0) c->ks.erase(name);
+        }
+        return rc;
+    }
     RBX_TRY(bitmap_for(c, name, size_bits(size), is_add, c->stream, &bm));
     if (!bm) {  // GETBIT on a missing key: every bit is 0
         if (out_flags) memset(out_flags, 0, keys->n);

@@ -192,6 +192,12 @@ void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const Filte
                                  const uint64_t *seg_off, uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax,
                                  uint8_t *out, unsigned long long *counts, hipStream_t st, bool slots);
 void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st);
+// |size| > 2^32 filters (k_wide_*): add = first-setter claim + resolve over a 2^tlog2-entry table
+// (all ~0 on entry); *oob = 1 when an index passes the Redis offset limit.  bm may be NULL for
+// contains (a missing key).
+void launch_bloom_wide(const KeysDev &keys, uint64_t m, uint32_t k, uint32_t *bm, unsigned long long *len,
+                       unsigned long long *table, uint32_t tlog2, bool is_add, uint8_t *out,
+                       unsigned long long *count, unsigned long long *oob, hipStream_t st);
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);
 // order-independent digest of a Redis string's bytes (replica comparison); *out += digest
 void launch_digest(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st);

@@ -5,7 +5,9 @@
   fill runs on the calling stream, after every earlier call of the context.
 - Handles outlive rbx_shutdown safely; every call on them then fails.
 - tryInit with a negative expectedInsertions (the reference accepts it,
-  M/RedissonBloomFilter.java:270-276): add / contains / count against the oracle.
+  M/RedissonBloomFilter.java:270-276): add / contains / count against the oracle, including
+  |size| > 2^32, where an index past the Redis offset limit makes the call throw RedisException
+  after the batch's other SETBITs ran (rbx.h RBX_E_REDIS).
 - Binary (NUL-containing) Bloom names through the *_n entry points.
 - Register pack / unpack_max, and an element-partitioned HLL set merged across two processes
   that created their HLLs in different orders (the exchange rbx_hll_allreduce_max performs with
@@ -19,7 +21,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from redisson_amd import Arena, BloomHandle, IllegalStateException, RedissonClient, device_keys
+from redisson_amd import Arena, BloomHandle, IllegalStateException, RedisException, RedissonClient, device_keys
 from redisson_amd import _lib as L
 from redisson_amd.client import _check
 
@@ -141,6 +143,72 @@ def test_negative_expected_insertions_filter(client, fresh):
     assert c == c_ref and np.array_equal(pres, pres_ref)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
+    f.delete()
+
+
+def _wide_call(f, ref, keys, is_add):
+    """one add / contains on the GPU and the oracle: both fail (-9 / RedisException) or both give
+    the same count and per-key flags"""
+    c_ref, fl_ref = (ref.add if is_add else ref.contains)(*O.arena(keys), per_key=True)
+    if c_ref == -9:
+        with pytest.raises(RedisException, match="bit offset is not an integer or out of range"):
+            (f.addEach if is_add else f.containsEach)(Arena(keys))
+        return False
+    c, fl = (f.addEach if is_add else f.containsEach)(Arena(keys))
+    assert c == c_ref and np.array_equal(fl, fl_ref)
+    return True
+
+
+def test_filter_past_the_redis_offset_limit(client, fresh):
+    """|size| = 4,792,529,188 (tryInit(-5e8, 0.01)): 10% of the indexes pass 2^32 - 1."""
+    f = client.getBloomFilter(fresh)
+    assert f.tryInit(-500_000_000, 0.01)
+    size, k = f.getSize(), f.getHashIterations()
+    assert (size, k) == O.bloom_optimal(-500_000_000, 0.01) and -size > (1 << 32)
+    ref = O.OracleBloom(size, k)
+    rng = np.random.default_rng(31)
+    # a batch made only of error replies creates no key: k = 1 over |size| = 1.44e12 bits
+    g = client.getBloomFilter(fresh + "-k1")
+    assert g.tryInit(-1_000_000_000_000, 0.5)
+    gs, gk = g.getSize(), g.getHashIterations()
+    assert gk == 1 and -gs > (300 << 32)
+    gref = O.OracleBloom(gs, gk)
+    lone = next(key for key in (rng.bytes(16) for _ in range(100))
+                if O.bloom_indexes(*O.redisson_hash128(key), gk, gs)[0] > 0xFFFFFFFF)
+    assert not _wide_call(g, gref, [lone], True)
+    assert _del(client, fresh + "-k1") == 0  # no bitmap key (the config stays)
+    g.delete()
+    ok = [_wide_call(f, ref, [rng.bytes(16)], True) for _ in range(48)]
+    assert 5 < sum(ok) < 43  # ~46% of single keys stay below the limit
+    assert not _wide_call(f, ref, [rng.bytes(24) for _ in range(3000)], True)  # throws, bits still set
+    seen = [rng.bytes(16) for _ in range(8)]
+    for key in seen:
+        _wide_call(f, ref, [key], True)
+    res = [_wide_call(f, ref, [key], False) for key in seen + [rng.bytes(16) for _ in range(24)]]
+    assert any(res) and not all(res)
+    assert not _wide_call(f, ref, seen * 50, False)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.count() == ref.count()
+    f.delete()
+
+
+def test_filter_just_past_2_32_bits(client, fresh):
+    """|size| = 2^32 + 7 (tryInit(-448,089,843, 0.01)): indexes mod |size| in 64 bits, and a batch
+    of 200K keys (with repeats) almost never reaches an offset past the limit -- per-key in-order
+    flags and presence against the oracle."""
+    f = client.getBloomFilter(fresh)
+    assert f.tryInit(-448_089_843, 0.01)
+    size, k = f.getSize(), f.getHashIterations()
+    assert -size == (1 << 32) + 7 and k == 7
+    ref = O.OracleBloom(size, k)
+    rng = np.random.default_rng(32)
+    base = [rng.bytes(int(n)) for n in rng.integers(0, 60, size=60_000)]
+    for _ in range(2):
+        batch = [base[int(j)] for j in rng.integers(0, len(base), size=100_000)]
+        assert _wide_call(f, ref, batch, True)
+    probe = base[:20_000] + [rng.bytes(33) for _ in range(20_000)]
+    assert _wide_call(f, ref, probe, False)
+    assert f.exportBitmap() == ref.redis_string()
     f.delete()
 
 

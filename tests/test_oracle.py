@@ -88,6 +88,36 @@ def test_bloom_indexes_python_vs_c():
             assert O.bloom_indexes(h1, h2, k, size) == P.bloom_indexes(h1, h2, k, size)
 
 
+def test_wide_size_offset_limit():
+    """|size| > 2^32 (tryInit with a negative expectedInsertions): a SETBIT / GETBIT past the Redis
+    offset limit 2^32 - 1 is an error reply; the batch's other SETBITs still run and the call then
+    throws (RedisException, -9).  Checked key by key against pyref's indexes."""
+    size, k = O.bloom_optimal(-500_000_000, 0.01)
+    assert size < -(1 << 32) and k == 7
+    rng = np.random.default_rng(17)
+    f = O.OracleBloom(size, k)
+    expect_bits, n_ok, n_err = set(), 0, 0
+    for i in range(64):
+        key = rng.bytes(16)
+        h1, h2 = P.highway_hash128(key)
+        idx = P.bloom_indexes(h1, h2, k, size)
+        oob = any(x > 0xFFFFFFFF for x in idx)
+        new = any(x <= 0xFFFFFFFF and x not in expect_bits for x in idx)
+        c = f.add(*O.arena([key]))
+        expect_bits.update(x for x in idx if x <= 0xFFFFFFFF)
+        if oob:
+            assert c == -9
+            n_err += 1
+        else:
+            assert c == int(new)
+            n_ok += 1
+        assert f.contains(*O.arena([key])) == (-9 if oob else 1)
+    assert n_ok > 5 and n_err > 5  # P(no index past the limit) = (2^32 / |size|)^7 ~ 0.46
+    bits = np.unpackbits(f.bitmap[: f.redis_len])
+    assert set(np.flatnonzero(bits).tolist()) == expect_bits
+    assert f.redis_len == max(expect_bits) // 8 + 1
+
+
 def test_java_math_round():
     assert O.java_math_round(0.49999999999999994) == 0
     assert O.java_math_round(0.5) == 1
