@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--add-fraction", type=float, default=0.1, help="C5 share of add commands")
     p.add_argument("--c5-replies", type=int, default=1,
                    help="C5: write every command's reply in the timed step (1, the metric) or not (0, A/B only)")
+    p.add_argument("--c5-fresh", type=int, default=1,
+                   help="C5: step s gives command i key i+s of a pool of n+W+K keys, so every step's (tenant, key) "
+                        "pairs are new (1), or replays the same stream each step (0)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline C2 sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-hostpath", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
@@ -781,15 +784,19 @@ def run_c5(args, world, rank, local, steps, warmup):
     u = torch.rand(n, dtype=torch.float64, device="cuda", generator=g)
     kf = torch.searchsorted(cdf, u).clamp_(max=nt - 1).to(torch.int32)
     op = (torch.rand(n, device="cuda", generator=g) < args.add_fraction).to(torch.uint8)
-    keys = torch.randint(0, 256, (n, 64), dtype=torch.uint8, device="cuda", generator=g)
+    extra = warmup + steps + 1 if args.c5_fresh else 0  # the key window slides one key per step
+    keys = torch.randint(0, 256, (n + extra, 64), dtype=torch.uint8, device="cuda", generator=g)
     counts = torch.zeros(2, dtype=torch.int64, device="cuda")
     # every command's reply (add(T): newly added, contains(T): present -- the booleans the reference
     # returns, M/RedissonBloomFilter.java:99-102,198-201) is written in the timed step
     replies = torch.empty(n, dtype=torch.uint8, device="cuda")
     arr = (C.c_void_p * nt)(*[h.h.value for h in handles])
-    dk = device_keys(keys.data_ptr(), n, 64)
+    windows = [device_keys(keys.data_ptr() + 64 * j, n, 64) for j in range(max(extra, 1))]
+    it = [0]
 
     def step():
+        dk = windows[it[0] % len(windows)]
+        it[0] += 1
         assert L.lib().rbx_bloom_stream_dev(client.ctx, arr, nt, kf.data_ptr(), op.data_ptr(), C.byref(dk),
                                              replies.data_ptr() if args.c5_replies else None, counts.data_ptr(),
                                              sptr) == 0
@@ -814,8 +821,8 @@ def run_c5(args, world, rank, local, steps, warmup):
     del tbl
     algo = n * (64 + 10 * 8 + 1)  # key + k x 8 B gathered + the 1-byte reply written
     # PMC counts of profiles/traffic.json are of the default workload's calls only
-    tj = args.traffic_json if (n, args.tenants, world, args.zipf_s, args.add_fraction) == \
-        (100_000_000, 100_000, 1, 1.0, 0.1) else None
+    tj = args.traffic_json if (n, args.tenants, world, args.zipf_s, args.add_fraction, args.c5_fresh) == \
+        (100_000_000, 100_000, 1, 1.0, 0.1, 1) else None
     res = {
         "metric": "Bloom mixed contains+add ops/sec (whole node), C5: 90/10 stream, Zipf tenants, 64-byte keys",
         "value": value, "unit": "ops/s", "n_gpus": world, "steps": steps, "warmup": warmup,
@@ -827,6 +834,8 @@ def run_c5(args, world, rank, local, steps, warmup):
                    "tenants_this_gpu": nt, "ops_per_gpu": n, "hottest_tenant_ops": top,
                    "replies": "one u8 reply per command written to HBM in every timed step" if args.c5_replies
                    else "NOT written (A/B run; not the metric)",
+                   "stream": "fresh per step: command i of step s takes key i+s (new (tenant, key) pairs)"
+                   if args.c5_fresh else "the same stream every step (adds after the first step re-set their bits)",
                    "parallelism": f"CRC16-slot sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
@@ -986,6 +995,9 @@ def main():
         key, val = kv.split("=")
         if key == "c5_replies":  # bench-side A/B switch (not an engine knob): C5 timed without replies
             args.c5_replies = int(val)
+            continue
+        if key == "c5_fresh":  # bench-side switch: a fresh stream per step (see --c5-fresh)
+            args.c5_fresh = int(val)
             continue
         assert L.lib().rbx_tune(key.encode(), int(val)) == 0, kv
     log(f"[bench] rank {rank}/{world} workload {args.workload}")

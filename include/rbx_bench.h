@@ -58,9 +58,15 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *                           2 auto (default: the call's bitmaps exceed 64 MiB)
  *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44
  *   "contains_qgrid"        slot kernel grid, 256..8192 (default 2048)
- *   "stream_contains_slots" ordered-stream contains: 0 staged kernel (default), 1 slot kernel
+ *   "stream_contains_slots" ordered-stream contains: 1 slot kernel (default), 0 staged kernel
  *   "stream_table8"         ordered stream's first-setter table: 1 (default) 8-byte entries claimed
  *                           by one CAS and committed by a table walk, 0 the 16-byte epoch-tagged table
+ *   "stream_prefilter"      ordered stream: 0 (default) every clear bit of a contains is looked up in
+ *                           the first-setter table; 16..27 = a 2^bits prefilter of the adds' zero
+ *                           bits gates the lookups (one atomicOr per zero bit)
+ *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
+ *                           the occupancy bitmap of the table's slots, 0 (default) = none
+ *   "stream_chunk"          ordered stream: commands per chunk cap (0 = default, 2^26 / k)
  *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
  *                           resident blocks (default 33000: four per CU; 0: registers decide)
  *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,

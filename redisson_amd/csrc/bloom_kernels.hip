@@ -624,6 +624,17 @@ __device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx, ui
     return (uint32_t)(((((uint64_t)fid << 32) | idx) * 0x9E3779B97F4A7C15ULL) >> pshift);
 }
 
+// May this clear bit have been set by an earlier add of the chunk (look it up in the table)?
+// pshift 0 (r04, with the 8-byte table): `filter` is the occupancy bitmap of the table's slots
+// (k_stream_occ) -- linear probing puts a key at or after its home slot, so an empty home slot
+// means the key is absent; else `filter` is the (fid, bit) prefilter the adds set; NULL: always.
+__device__ __forceinline__ bool maybe_claimed(const uint32_t *__restrict__ filter, uint32_t pshift, uint32_t fid,
+                                              uint32_t idx, uint64_t key8, uint32_t lg8) {
+    if (!filter) return true;
+    const uint64_t b = pshift ? (uint64_t)prefilter_bit(fid, idx, pshift) : t8_slot(key8, lg8);
+    return (filter[b >> 5] >> (b & 31)) & 1u;
+}
+
 // adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
 __global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restrict__ op, uint64_t base, uint64_t nchunk,
                                                         uint32_t *__restrict__ adds, uint32_t *__restrict__ nadds) {
@@ -744,9 +755,8 @@ __global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t 
 #pragma unroll
             for (int u = 0; u < KMAX; ++u) {
                 if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
-                    // set by an earlier add of this chunk?  Only possible if the prefilter says so.
-                    const uint32_t pfb = prefilter_bit(f.fid, idxs[u], pshift);
-                    if (!prefilter || ((prefilter[pfb >> 5] >> (pfb & 31)) & 1u)) {
+                    // set by an earlier add of this chunk?  Only possible if the filter says so.
+                    if (maybe_claimed(prefilter, pshift, f.fid, idxs[u], ((uint64_t)f.fid << bb) | idxs[u], lg8)) {
                         const uint32_t owner = T8 ? t8_find(T8, lg8, pb, ((uint64_t)f.fid << bb) | idxs[u])
                                                   : ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
                         all = owner < (uint32_t)t;
@@ -885,9 +895,8 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
             bool fin_p = false;
             if (act[s]) {
                 bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
-                if (clear) {  // set by an earlier add of this chunk?  Only if the prefilter says so.
-                    const uint32_t pfb = prefilter_bit(sfid[s], sidx[s], pshift);
-                    if (!prefilter || ((prefilter[pfb >> 5] >> (pfb & 31)) & 1u))
+                if (clear) {  // set by an earlier add of this chunk?  Only if the filter says so.
+                    if (maybe_claimed(prefilter, pshift, sfid[s], sidx[s], ((uint64_t)sfid[s] << bb) | sidx[s], lg8))
                         clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
                                       : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
                 }
@@ -991,13 +1000,27 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
         for (int j = 0; j < KMAX; ++j) {
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
                 t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
-                if (prefilter) {
+                if (prefilter && pshift) {  // pshift 0: occupancy bitmap, built by k_stream_occ
                     const uint32_t pb2 = prefilter_bit(f.fid, idxs[j], pshift);
                     atomicOr(&prefilter[pb2 >> 5], 1u << (pb2 & 31));
                 }
             }
         }
         raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+// the occupancy bitmap of the table's 2^lg slots (bit s = slot s holds an entry), one ballot per 64
+// slots: streamed after the probe, no atomics (the r03 prefilter cost a memory-side atomicOr per
+// zero bit).  lg >= 12, so every wave's 64 slots exist.
+__global__ __launch_bounds__(256) void k_stream_occ(const unsigned long long *__restrict__ T,
+                                                    const uint32_t *__restrict__ nadds, uint32_t kmax,
+                                                    uint32_t *__restrict__ occ) {
+    const uint64_t nslots = 1ULL << t8_log2(*nadds, kmax);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s - (threadIdx.x & 63) < nslots; s += stride) {
+        const uint64_t m = __ballot(T[s] != ~0ULL);
+        if ((threadIdx.x & 63) == 0) ((unsigned long long *)occ)[s >> 6] = m;
     }
 }
 
@@ -1454,6 +1477,8 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
+    if (a.t8 && a.prefilter && a.pshift == 0)  // occupancy filter of the 8-byte table
+        hipLaunchKernelGGL(k_stream_occ, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.kmax, a.prefilter);
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
                            a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,

@@ -187,6 +187,7 @@ struct rbx_ctx {
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf pa_stamps;  // add_partition_diag & 64: region-pass phase times (rbx_bench_add_stamps)
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
+    DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
     DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
     uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
@@ -887,7 +888,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs, &c->wide_table}) {
+                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -1597,10 +1598,21 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
 // Ordered mixed stream (C5): see rbx.h.  Chunks of <= 2^26 pairs run probe -> contains -> commit.
 // rbx_tune("stream_chunk", n) caps a chunk at n commands (tests: many chunks on small streams).
 static uint64_t g_stream_chunk = 0;
-// rbx_tune("stream_prefilter"): pbits in [20, 27] = the adds also set a 2^pbits-bit prefilter that a
-// contains reads before it looks a clear bit up in the first-setter table (default 23: 1 MiB);
-// 0 = the table alone (measured slower: 10.3 -> 10.8 ms per 1e8 C5 commands)
-static int g_stream_prefilter = 23;
+// rbx_tune("stream_prefilter"): pbits in [16, 27] = the adds also set a 2^pbits-bit prefilter that a
+// contains reads before it looks a clear bit up in the first-setter table; 0 (default since r04) =
+// the table alone.  With the 8-byte table (64 MiB for a C5 chunk) a lookup costs less than the
+// prefilter's memory-side atomicOr per zero bit: C5 with new (tenant, key) pairs every step 17.0 /
+// 17.1 ms per 1e8 commands vs 17.8 / 17.9 at 2^23 bits, 17.2 / 17.3 at 2^25, 18.4 at 2^22
+// (profiles/r04/r04g_c5_fresh_prefilter.jsonl).  A replayed stream (adds that find no zero bit) is
+// the one case a prefilter pays: 10.2 ms at 2^23 vs 10.8 without.
+static int g_stream_prefilter = 0;
+// rbx_tune("stream_occupancy"): 1 = without a prefilter, a clear bit is looked up in the 8-byte
+// table only when its home slot is occupied (a bitmap of the table's slots, streamed from the table
+// after the probe: k_stream_occ, no atomics); 0 (default) = every clear bit looked up.  Measured
+// slower on the fresh C5 stream: 17.62 / 17.67 / 17.64 vs 17.29 / 17.20 ms per 1e8 commands
+// (profiles/r04/r04o_c5_occupancy_rejected.jsonl): the 64 MiB table's lookups cost less than the
+// extra pass and the bitmap's L2 footprint.
+static int g_stream_occ = 0;
 // rbx_tune("stream_table8"): 1 (default) the 8-byte first-setter table + walk commit (r04) when
 // (fid, bit) fits 41 bits, 0 the r03 16-byte epoch-tagged table
 static int g_stream_table8 = 1;
@@ -1646,6 +1658,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             HIP_TRY(hipMemsetAsync(c->st_t8.p, 0xff, entries * 8, st));
             c->st_t8_entries = entries;
         }
+        RBX_TRY(c->st_occ.reserve(entries / 8));  // written whole by k_stream_occ before it is read
         if (c->st_flag_bytes < chunk) {
             c->st_flag_bytes = 0;
             RBX_TRY(c->st_flag.reserve(chunk));
@@ -1673,6 +1686,10 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
         } else {
             HIP_TRY(hipMemsetAsync(s.nadds, 0, 4, st));
             s.prefilter = nullptr;
+            if (t8 && g_stream_occ) {  // the table's slot-occupancy bitmap (k_stream_occ), pshift 0
+                s.prefilter = c->st_occ.as<uint32_t>();
+                s.pshift = 0;
+            }
         }
         s.keys = keys;
         s.base = base;
@@ -3157,9 +3174,14 @@ int rbx_tune(const char *key, int value) {
         g_stream_chunk = (uint64_t)value;
         return RBX_OK;
     }
+    if (!strcmp(key, "stream_occupancy")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_occupancy: 0 or 1");
+        g_stream_occ = value;
+        return RBX_OK;
+    }
     if (!strcmp(key, "stream_prefilter")) {
-        if (value != 0 && (value < 20 || value > 27))
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_prefilter: 0 or bits in [20, 27]");
+        if (value != 0 && (value < 16 || value > 27))
+            return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_prefilter: 0 or bits in [16, 27]");
         g_stream_prefilter = value;
         return RBX_OK;
     }

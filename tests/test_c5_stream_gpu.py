@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 # the engine's defaults (rbx_bench.h rbx_tune), restored after a case that overrides them
 STREAM_SLOTS_DEFAULT = 1
-STREAM_PREFILTER_DEFAULT = 23
+STREAM_PREFILTER_DEFAULT = 0
 
 
 def _zipf_tenants(rng, nt, n, s=1.0):
@@ -30,7 +30,8 @@ def _zipf_tenants(rng, nt, n, s=1.0):
     return np.minimum(np.searchsorted(cdf, rng.random(n)), nt - 1).astype(np.uint32)
 
 
-def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None):
+def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
+             occupancy=None):
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
@@ -63,6 +64,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_prefilter", prefilter) == 0
     if table8 is not None:
         assert L.lib().rbx_tune(b"stream_table8", table8) == 0
+    if occupancy is not None:
+        assert L.lib().rbx_tune(b"stream_occupancy", occupancy) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
     finally:
@@ -70,6 +73,7 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         L.lib().rbx_tune(b"stream_contains_slots", STREAM_SLOTS_DEFAULT)
         L.lib().rbx_tune(b"stream_prefilter", STREAM_PREFILTER_DEFAULT)
         L.lib().rbx_tune(b"stream_table8", 1)
+        L.lib().rbx_tune(b"stream_occupancy", 0)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -119,6 +123,16 @@ def test_c5_first_setter_tables_agree(client, fresh, table8):
              table8=table8)
 
 
+@pytest.mark.parametrize("occupancy", [0, 1])
+@pytest.mark.parametrize("slots", [0, 1])
+def test_c5_table_occupancy_filter(client, fresh, occupancy, slots):
+    """Without a prefilter, a clear bit is looked up in the 8-byte first-setter table only when its
+    home slot is occupied (k_stream_occ's bitmap, 1) or always (0, default): both contains kernels,
+    small chunks (many occupancy passes), exact against the oracle."""
+    _c5_case(client, fresh, seed=515 + 2 * occupancy + slots, nt=150, expected=1_000_000, fpp=1e-3, n=1_200_000,
+             chunk=200_000, slots=slots, prefilter=0, occupancy=occupancy)
+
+
 def test_c5_k10_chunk_boundaries(client, fresh):
     """C5 tenants and keys in 303,031-command chunks (= 101 * 3000 + 1: the add at 303,030 and the
     contains of the same key at 303,031 sit on the two sides of the first boundary; the earlier
@@ -132,7 +146,7 @@ def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, prefilter):
     filter's index in the call (up to 2^17 here), so the bench leg's id range is checked against the
     oracle too: 100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10 -> the same <64, 16>
     instantiation as C5, 1.8 KB each), Zipf(1.0) tenants, 10% adds, 64-byte keys, 2.1M commands in
-    three chunks, with the prefilter (default 2^23 bits) and without it (every clear bit looked up in
+    three chunks, with a 2^23-bit prefilter and without it (the default) (every clear bit looked up in
     the table).  Per-command replies, both counts and every tenant's bitmap must be identical."""
     f = client.getBloomFilter(fresh + "-probe")
     f.tryInit(1000, 1e-3)
