@@ -67,6 +67,8 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
  *                           the occupancy bitmap of the table's slots, 0 (default) = none
  *   "stream_chunk"          ordered stream: commands per chunk cap (0 = default, 2^26 / k)
+ *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-
+ *                           slot CAS) all in flight at once, 0 one after another
  *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
  *                           resident blocks (default 33000: four per CU; 0: registers decide)
  *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,

@@ -973,7 +973,8 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
                                                        const FilterDesc *__restrict__ filt,
                                                        const uint32_t *__restrict__ kf, unsigned long long *__restrict__ T,
                                                        uint32_t bb, uint32_t pb, uint32_t kmax,
-                                                       uint32_t *__restrict__ prefilter, uint32_t pshift) {
+                                                       uint32_t *__restrict__ prefilter, uint32_t pshift,
+                                                       uint32_t batch) {
     const uint32_t na = *nadds;
     const uint32_t lg = t8_log2(na, kmax);
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -996,11 +997,49 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
             }
             h += (j & 1) ? h1 : h2;
         }
+        // the zero bits' claims: every home-slot CAS in flight at once (a C5 add of the fresh stream
+        // meets ~5 zero bits; one CAS round trip after another was a serial chain per lane), then
+        // the rare occupied home slot of another bit probes on serially
+        uint32_t zm = 0;
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
-                t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
-                if (prefilter && pshift) {  // pshift 0: occupancy bitmap, built by k_stream_occ
+        for (int j = 0; j < KMAX; ++j)
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
+        if (batch) {
+            const uint64_t mask = (1ULL << lg) - 1;
+            unsigned long long old[KMAX];
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if (zm & (1u << j)) {
+                    const uint64_t key = ((uint64_t)f.fid << bb) | idxs[j];
+                    old[j] = atomicCAS(&T[t8_slot(key, lg)], ~0ULL, ((unsigned long long)key << pb) | t);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if (!(zm & (1u << j)) || old[j] == ~0ULL) continue;
+                const uint64_t key = ((uint64_t)f.fid << bb) | idxs[j];
+                const unsigned long long mine = ((unsigned long long)key << pb) | t;
+                uint64_t slot = t8_slot(key, lg);
+                unsigned long long o = old[j];
+                for (uint64_t probes = 0; probes <= mask; ++probes) {
+                    if (o == ~0ULL) break;
+                    if ((o >> pb) == key) {
+                        if (o > mine) atomicMin(&T[slot], mine);
+                        break;
+                    }
+                    slot = (slot + 1) & mask;
+                    o = atomicCAS(&T[slot], ~0ULL, mine);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j)
+                if (zm & (1u << j)) t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
+        }
+        if (prefilter && pshift) {  // pshift 0: occupancy bitmap, built by k_stream_occ
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if (zm & (1u << j)) {
                     const uint32_t pb2 = prefilter_bit(f.fid, idxs[j], pshift);
                     atomicOr(&prefilter[pb2 >> 5], 1u << (pb2 & 31));
                 }
@@ -1464,6 +1503,10 @@ static unsigned g_stream_qgrid = 1024;
 // rbx_tune("stream_contains_lds") overrides the bytes (0: registers decide).
 static int g_stream_lds = 33000;
 void set_stream_contains_lds(int v) { g_stream_lds = v; }
+// k_stream_probe8: 1 (default) every zero bit's home-slot CAS issued before any is waited on, 0 one
+// claim after another (rbx_tune "stream_probe_batch")
+static uint32_t g_probe8_batch = 1;
+void set_stream_probe_batch(int v) { g_probe8_batch = (uint32_t)v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1473,7 +1516,7 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                        a.nadds);
     if (a.t8)
         hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.t8, a.bb, a.pb, a.kmax, a.prefilter, a.pshift);
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.kmax, a.prefilter, a.pshift, g_probe8_batch);
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);

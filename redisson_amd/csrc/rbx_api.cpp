@@ -3195,6 +3195,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_qgrid(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "stream_probe_batch")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_probe_batch: 0 or 1");
+        set_stream_probe_batch(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "stream_contains_lds")) {
         if (value < 0 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_contains_lds in [0, 65536]");
         set_stream_contains_lds(value);

@@ -31,7 +31,7 @@ def _zipf_tenants(rng, nt, n, s=1.0):
 
 
 def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
-             occupancy=None):
+             occupancy=None, probe_batch=None):
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
@@ -66,6 +66,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_table8", table8) == 0
     if occupancy is not None:
         assert L.lib().rbx_tune(b"stream_occupancy", occupancy) == 0
+    if probe_batch is not None:
+        assert L.lib().rbx_tune(b"stream_probe_batch", probe_batch) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
     finally:
@@ -74,6 +76,7 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         L.lib().rbx_tune(b"stream_prefilter", STREAM_PREFILTER_DEFAULT)
         L.lib().rbx_tune(b"stream_table8", 1)
         L.lib().rbx_tune(b"stream_occupancy", 0)
+        L.lib().rbx_tune(b"stream_probe_batch", 1)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -113,6 +116,15 @@ def test_c5_kmax8_many_chunks(client, fresh, slots, prefilter):
     prefilter in front of the first-setter table."""
     _c5_case(client, fresh, seed=77 + slots + 2 * prefilter, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000,
              chunk=300_000, slots=slots, prefilter=prefilter)
+
+
+@pytest.mark.parametrize("probe_batch", [0, 1])
+def test_c5_probe_claims_batched_or_serial(client, fresh, probe_batch):
+    """The 8-byte table's claims: every home-slot CAS of an add in flight at once (1, default) or one
+    after another (0); hot tenants (Zipf, 120 of them) make shared bits and occupied home slots
+    common within a chunk, so the atomicMin and the serial probe-on paths both run."""
+    _c5_case(client, fresh, seed=616 + probe_batch, nt=120, expected=1_000_000, fpp=1e-3, n=1_400_000,
+             chunk=350_000, probe_batch=probe_batch)
 
 
 @pytest.mark.parametrize("table8", [0, 1])
