@@ -1632,7 +1632,18 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     if (d_keys->n == 0) return RBX_OK;
     KeysDev keys = keys_dev(d_keys);
     const uint64_t k = std::max<uint32_t>(kmax, 1);
-    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, (1ULL << 26) / k));
+    // r04: 8-byte first-setter entries when (fid, bit) leaves >= 23 bits for a chunk position
+    uint32_t bb = 1, fbits = 0;
+    while ((1ULL << bb) < c->filt_maxbits) ++bb;
+    while ((1ULL << fbits) < c->filt_nfids) ++fbits;
+    const bool t8 = g_stream_table8 && bb + fbits <= 41;
+    const uint32_t pb = 64 - bb - fbits;
+    // Chunks: <= 2^26 (add, bit) pairs for the 16-byte table; with 8-byte entries as many commands
+    // as a position field holds, <= 2^27 pairs (a worst-case table of <= 1-2 GiB): C5 8.4M commands
+    // per chunk instead of 6.7M -- larger chunks amortise the per-chunk passes (fresh C5: 3.4M /
+    // 1.7M-command chunks 18.5 / 20.3 ms vs 17.0 at 6.7M, profiles/r04/r04c_c5_chunk.jsonl)
+    const uint64_t cap8 = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, (1ULL << 27) / k);
+    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, t8 ? cap8 : (1ULL << 26) / k));
     // chunk bases on 128-command boundaries keep the replies' range images line-aligned
     if (chunk < keys.n && chunk > 128) chunk &= ~127ULL;
     if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
@@ -1642,15 +1653,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     const uint64_t kPrefilterWords = 1ULL << (pbits - 5);
     RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
     const int fl = fast_len(keys);
-    // r04: 8-byte first-setter entries when (fid, bit) leaves >= 23 bits for a chunk position
-    uint32_t bb = 1, fbits = 0;
-    while ((1ULL << bb) < c->filt_maxbits) ++bb;
-    while ((1ULL << fbits) < c->filt_nfids) ++fbits;
-    const bool t8 = g_stream_table8 && bb + fbits <= 41;
-    const uint32_t pb = 64 - bb - fbits;
     if (t8) {
-        const uint64_t cap = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, 1ULL << 30);
-        if (chunk > cap) chunk = cap > 128 ? cap & ~127ULL : cap;
         const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)k);
         if (c->st_t8_entries < entries) {
             c->st_t8_entries = 0;

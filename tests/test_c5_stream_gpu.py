@@ -100,12 +100,13 @@ def _fixed(keys):
 
 def test_c5_instantiation_two_full_chunks(client, fresh):
     """C5 exactly: tryInit(1e6, 1e-3) tenants (14,377,587 bits, k = 10 -> k_stream_*<64, 16>), 64-byte
-    keys, 7M commands = two chunks at the production chunk size (2^26 / 10 = 6,710,886 commands)."""
+    keys, 14M commands = two chunks at the production chunk size (8-byte table: 2^27 / 10 rounded to
+    128 = 13,421,696 commands for 200 tenants; C5's 100k tenants get 2^23 - 128)."""
     f = client.getBloomFilter(fresh + "-probe")
     f.tryInit(1_000_000, 1e-3)
     assert (f.getSize(), f.getHashIterations()) == (14_377_587, 10)
     f.delete()
-    _c5_case(client, fresh, seed=0x5EED0005, nt=200, expected=1_000_000, fpp=1e-3, n=7_000_000)
+    _c5_case(client, fresh, seed=0x5EED0005, nt=200, expected=1_000_000, fpp=1e-3, n=14_000_000)
 
 
 @pytest.mark.parametrize("prefilter", [0, 21, 25])
