@@ -1516,22 +1516,22 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                        a.nadds);
     if (a.t8)
         hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.t8, a.bb, a.pb, a.kmax, a.prefilter, a.pshift, g_probe8_batch);
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.prefilter, a.pshift, g_probe8_batch);
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
     if (a.t8 && a.prefilter && a.pshift == 0)  // occupancy filter of the 8-byte table
-        hipLaunchKernelGGL(k_stream_occ, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.kmax, a.prefilter);
+        hipLaunchKernelGGL(k_stream_occ, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.prefilter);
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
                            a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
-                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.kmax, a.nadds);
+                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
-                           a.t8, a.bb, a.pb, a.kmax, a.nadds);
+                           a.t8, a.bb, a.pb, a.tkmax, a.nadds);
     if (a.t8) {
-        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.kmax, a.bb, a.pb, a.fid_bm,
+        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
                            a.flag);
         hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);
     } else {

@@ -1616,6 +1616,9 @@ static int g_stream_occ = 0;
 // rbx_tune("stream_table8"): 1 (default) the 8-byte first-setter table + walk commit (r04) when
 // (fid, bit) fits 41 bits, 0 the r03 16-byte epoch-tagged table
 static int g_stream_table8 = 1;
+// rbx_tune("stream_table_scale"): 1, 2 or 4 -- the 8-byte table holds 2^t8_log2(adds x k x scale)
+// entries (scale 1: load <= 8/9 if every bit of every add were 0)
+static int g_stream_table_scale = 1;
 int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
                          const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
                          unsigned long long *d_counts, void *stream) {
@@ -1640,8 +1643,10 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     const uint32_t pb = 64 - bb - fbits;
     // Chunks: <= 2^26 (add, bit) pairs for the 16-byte table; with 8-byte entries as many commands
     // as a position field holds, <= 2^27 pairs (a worst-case table of <= 1-2 GiB): C5 8.4M commands
-    // per chunk instead of 6.7M -- larger chunks amortise the per-chunk passes (fresh C5: 3.4M /
-    // 1.7M-command chunks 18.5 / 20.3 ms vs 17.0 at 6.7M, profiles/r04/r04c_c5_chunk.jsonl)
+    // per chunk instead of 6.7M.  What that bought (fresh C5, 16.2 vs 17.0 ms) is the table's load:
+    // 838K adds size it at 2^24 entries (~27% used) where 671K gave 2^23 (~43%); 6.7M-command chunks
+    // on a 2^24 table run as fast (16.34 / 16.41 vs 16.60 / 16.54 ms, r04l_c5_chunk_vs_table_load),
+    // larger tables again slower (r04s_c5_table_scale).  Smaller chunks: 3.4M / 1.7M 18.5 / 20.3 ms.
     const uint64_t cap8 = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, (1ULL << 27) / k);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, t8 ? cap8 : (1ULL << 26) / k));
     // chunk bases on 128-command boundaries keep the replies' range images line-aligned
@@ -1654,7 +1659,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
     const int fl = fast_len(keys);
     if (t8) {
-        const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)k);
+        const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)(k * g_stream_table_scale));
         if (c->st_t8_entries < entries) {
             c->st_t8_entries = 0;
             RBX_TRY(c->st_t8.reserve(entries * 8));
@@ -1678,6 +1683,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             s.bb = bb;
             s.pb = pb;
             s.fid_bm = c->fid_table.as<uint32_t *>();
+            s.tkmax = kmax * (uint32_t)g_stream_table_scale;
             s.flag = c->st_flag.as<uint8_t>();
         }
         s.adds = c->st_adds.as<uint32_t>();
@@ -3175,6 +3181,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "stream_chunk")) {
         if (value < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_chunk >= 0 (0: 2^26 / k commands)");
         g_stream_chunk = (uint64_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_table_scale")) {
+        if (value != 1 && value != 2 && value != 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_table_scale in {1, 2, 4}");
+        g_stream_table_scale = value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_occupancy")) {

@@ -170,6 +170,7 @@ struct StreamChunkArgs {
     // chunk's add count on the device; k_stream_walk commits it and restores every entry to EMPTY.
     unsigned long long *t8;
     uint32_t bb, pb;              // bits of the largest bitmap's bit index / of a chunk position
+    uint32_t tkmax;               // sizes the table: 2^t8_log2(*nadds, tkmax), tkmax = kmax x table scale
     uint32_t *const *fid_bm;      // bitmap words per table id (fid)
     uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks)
 };

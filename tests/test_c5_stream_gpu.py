@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 # the engine's defaults (rbx_bench.h rbx_tune), restored after a case that overrides them
 STREAM_SLOTS_DEFAULT = 1
 STREAM_PREFILTER_DEFAULT = 0
+STREAM_TABLE_SCALE_DEFAULT = 1
 
 
 def _zipf_tenants(rng, nt, n, s=1.0):
@@ -31,7 +32,7 @@ def _zipf_tenants(rng, nt, n, s=1.0):
 
 
 def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
-             occupancy=None, probe_batch=None):
+             occupancy=None, probe_batch=None, table_scale=None):
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
@@ -68,6 +69,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_occupancy", occupancy) == 0
     if probe_batch is not None:
         assert L.lib().rbx_tune(b"stream_probe_batch", probe_batch) == 0
+    if table_scale is not None:
+        assert L.lib().rbx_tune(b"stream_table_scale", table_scale) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
     finally:
@@ -77,6 +80,7 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         L.lib().rbx_tune(b"stream_table8", 1)
         L.lib().rbx_tune(b"stream_occupancy", 0)
         L.lib().rbx_tune(b"stream_probe_batch", 1)
+        L.lib().rbx_tune(b"stream_table_scale", STREAM_TABLE_SCALE_DEFAULT)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -126,6 +130,14 @@ def test_c5_probe_claims_batched_or_serial(client, fresh, probe_batch):
     common within a chunk, so the atomicMin and the serial probe-on paths both run."""
     _c5_case(client, fresh, seed=616 + probe_batch, nt=120, expected=1_000_000, fpp=1e-3, n=1_400_000,
              chunk=350_000, probe_batch=probe_batch)
+
+
+@pytest.mark.parametrize("scale", [1, 2, 4])
+def test_c5_table_scale(client, fresh, scale):
+    """The 8-byte table at 1x / 2x / 4x its entries (rbx_tune stream_table_scale): claims, lookups and
+    the walk follow the same 2^t8_log2 on every kernel; exact against the oracle."""
+    _c5_case(client, fresh, seed=717 + scale, nt=100, expected=1_000_000, fpp=1e-3, n=900_000, chunk=300_000,
+             table_scale=scale)
 
 
 @pytest.mark.parametrize("table8", [0, 1])
