@@ -963,7 +963,7 @@ __global__ __launch_bounds__(256) void k_stream_commit(KeysDev keys, uint64_t ba
 // read and owner lookup per zero bit.  Here an entry is ONE word, (fid << bb | bit) << pb | position:
 // a zero bit is claimed by one CAS on an empty slot (a slot already holding the bit takes an
 // atomicMin -- same high bits, so the minimum is the first setter), the table is sized to the
-// chunk's adds (2^t8_log2 entries, e.g. 8M = 64 MiB for C5's 671K adds), and the commit is a
+// chunk's adds (2^t8_log2 entries, e.g. 16M = 128 MiB for a C5 chunk's 838K adds), and the commit is a
 // streaming walk over it: every entry is an owned bit (its minimum position is the first add that
 // meets it at 0), so the walk ORs the bit into its bitmap, flags its owner and empties the slot.
 // A final pass over the add list turns the flags into replies and the new-add count.
