@@ -224,14 +224,27 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
         uint32_t parent, part, m;
         uint64_t start;
     };
-    auto find_item = [&](uint32_t from, Item &ii) -> uint32_t {  // uniform: the next item with pairs
-        for (uint32_t item = from; item < nitems; item += gridDim.x) {
-            const uint32_t it = item / nparts, ix = item - it * nparts;
-            ii.parent = ix % nparents;
-            ii.part = ii.parent * sub_div + ix / nparents;
-            const uint64_t nc = min<uint64_t>(cnt_in[ii.part], cap_in);
-            ii.start = (uint64_t)it * TILE;
-            if (ii.start < nc) {
+    // uniform: the next item with pairs.  64 candidate items per round, one per lane, so a small
+    // batch (C1: 7M pairs in items sized for the worst case) does not walk its empty items one
+    // dependent count load after another (C1's rebucket ~96 us per 1M-key add)
+    auto find_item = [&](uint32_t from, Item &ii) -> uint32_t {
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint32_t base = from; base < nitems; base += 64 * gridDim.x) {
+            const uint32_t cand = base + lane * gridDim.x;
+            bool has = false;
+            if (cand < nitems) {
+                const uint32_t it = cand / nparts, ix = cand - it * nparts;
+                const uint32_t part = (ix % nparents) * sub_div + ix / nparents;
+                has = (uint64_t)it * TILE < min<uint64_t>(cnt_in[part], cap_in);
+            }
+            const uint64_t hit = __ballot(has);
+            if (hit) {
+                const uint32_t item = base + (uint32_t)__builtin_ctzll(hit) * gridDim.x;
+                const uint32_t it = item / nparts, ix = item - it * nparts;
+                ii.parent = ix % nparents;
+                ii.part = ii.parent * sub_div + ix / nparents;
+                const uint64_t nc = min<uint64_t>(cnt_in[ii.part], cap_in);
+                ii.start = (uint64_t)it * TILE;
                 ii.m = (uint32_t)min<uint64_t>(TILE, nc - ii.start);
                 return item;
             }
