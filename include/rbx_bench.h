@@ -67,6 +67,7 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
  *                           the occupancy bitmap of the table's slots, 0 (default) = none
  *   "stream_chunk"          ordered stream: commands per chunk cap (0 = default, 2^26 / k)
+ *   "stream_qgrid"          ordered-stream slot contains kernel grid, 256..8192 (default 1024)
  *   "stream_table_scale"    ordered stream, 8-byte table entries x 1 (default), 2 or 4
  *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-
  *                           slot CAS) all in flight at once, 0 one after another

@@ -1495,6 +1495,7 @@ void set_stream_slots(int v) { g_stream_slots = v; }
 // resident round: C5 9.91 (2048) -> 9.67 ms; shapes 32 / 42 / 24: 10.8 / 11.2 / 11.2 ms
 // (profiles/r03/r03u_c5sweep_qshape_qgrid.jsonl).
 static unsigned g_stream_qgrid = 1024;
+void set_stream_qgrid(int v) { g_stream_qgrid = (unsigned)v; }
 // k_stream_contains runs best at four 256-thread blocks per CU (4 waves/SIMD): the Zipf-hot
 // tenants' bitmaps live in L2, and more resident waves interleave more tenants.  Its registers
 // (93 VGPRs since the r02 hash) would admit five, so the launch reserves 33,000 bytes of dynamic

@@ -3209,6 +3209,11 @@ int rbx_tune(const char *key, int value) {
         set_contains_qgrid(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "stream_qgrid")) {
+        if (value < 256 || value > 8192) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_qgrid in [256, 8192]");
+        set_stream_qgrid(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "stream_probe_batch")) {
         if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_probe_batch: 0 or 1");
         set_stream_probe_batch(value);
