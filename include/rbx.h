@@ -224,7 +224,11 @@ int rbx_bloom_handle_config(const rbx_bloom *b, uint64_t *size, uint32_t *k);
 /* contains over device-resident keys; *d_count += present keys (device word). */
 int rbx_bloom_contains_dev(rbx_ctx *ctx, rbx_bloom *b, const rbx_keys *d_keys,
                            uint8_t *d_out_present, unsigned long long *d_count, void *stream);
-/* add over device-resident keys; *d_count += newly added keys (device word). */
+/* add over device-resident keys; *d_count += newly added keys (device word).
+ * Exception to the *_dev convention: a large batch on a large filter (the region-partitioned add,
+ * bitmap >= 8 MiB and >= max(2^17, bits / 2^12) keys) waits on the stream once per chunk of up to
+ * ~55M keys, for the chunk's bucket-overflow flag -- an adversarial batch (one key repeated ~1e5
+ * times) reruns that chunk on the first-setter table path before the next chunk starts. */
 int rbx_bloom_add_dev(rbx_ctx *ctx, rbx_bloom *b, const rbx_keys *d_keys, uint8_t *d_out_new,
                       unsigned long long *d_count, void *stream);
 /* Multi-tenant batch: segment s = keys [seg_offsets[s], seg_offsets[s+1]) tested
