@@ -747,6 +747,10 @@ def run_c3(args, world, rank, local, steps, warmup):
 # ------------------------------------------------------------------------------------------
 # C5: ordered 90/10 contains/add stream, Zipf(1.0) tenants over the C3 set, 64-byte keys
 # ------------------------------------------------------------------------------------------
+# the kernels one default C5 call runs per chunk (rbx_bloom_stream_dev with the default tuning)
+C5_KERNELS = "k_stream_compact + k_stream_probe8 + k_stream_contains_q + k_stream_walk + k_stream_final"
+
+
 def run_c5(args, world, rank, local, steps, warmup):
     import ctypes as C
 
@@ -819,7 +823,10 @@ def run_c5(args, world, rank, local, steps, warmup):
     peak = max(segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), 1_797_199, 1, n, stream),
                gather_peak(client, 512 << 20, n, 7, stream, g))
     del tbl
-    algo = n * (64 + 10 * 8 + 1)  # key + k x 8 B gathered + the 1-byte reply written
+    nadds = int(op.sum().item())
+    # a contains = 64 B key + k x 8 B gathered = 144 B, an add +80 B RMW (k x 8 B); plus
+    # the 1-byte reply every command writes
+    algo = n * (64 + 10 * 8 + 1) + nadds * 10 * 8
     # PMC counts of profiles/traffic.json are of the default workload's calls only
     tj = args.traffic_json if (n, args.tenants, world, args.zipf_s, args.add_fraction, args.c5_fresh) == \
         (100_000_000, 100_000, 1, 1.0, 0.1, 1) else None
@@ -841,7 +848,8 @@ def run_c5(args, world, rank, local, steps, warmup):
                      "unit": "GB/s", "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": load_traffic(tj, "stream_pipeline", "hbm_bytes_by_class") or
                      load_traffic(tj, "stream_pipeline"),
-                     "kernel": "k_stream_compact + k_stream_probe + k_stream_contains_q + k_stream_commit", "kernel_avg_ms": ms,
+                     "kernel": C5_KERNELS, "kernel_avg_ms": ms,
+                     "algorithmic_bytes_per_launch": algo, "adds_per_launch": nadds,
                      "request_peak_kind": "max(k_gather_segments one key per tenant slice, k_gather_probe "
                                           "over 512 MiB) for reads; k_stream_write for writes",
                      **request_fields(tj, "stream_pipeline", ms, peak,

@@ -36,6 +36,11 @@ int rbx_bench_stream_write(rbx_ctx *ctx, void *d_buf, uint64_t bytes, void *stre
  * random 4-byte loads inside it. */
 int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_bytes, uint64_t segment_bytes,
                               uint64_t keys_per_segment, uint64_t nkeys, void *d_sink, void *stream);
+/* The ordered stream's 8-byte first-setter entry layout of the context's last rbx_bloom_stream[_dev]
+ * call: out[0] = bb (bitmap-index bits of the call's largest filter), out[1] = fbits (filter-id
+ * bits), out[2] = pb = 64 - bb - fbits (chunk-position bits; 0 when the 16-byte table ran),
+ * out[3] = commands per chunk.  Tests pin the production packing with it. */
+int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
 /* Process-wide tuning knobs (results never change; A/B runs and tests only):
  *   "contains_stage1"       early-exit schedule of contains: 0 = all k gathers at once,
  *                           1..3 = that many bits first, 4 = doubling 1,2,4,... (default),
@@ -66,7 +71,10 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  *                           bits gates the lookups (one atomicOr per zero bit)
  *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
  *                           the occupancy bitmap of the table's slots, 0 (default) = none
- *   "stream_chunk"          ordered stream: commands per chunk cap (0 = default, 2^26 / k)
+ *   "stream_chunk"          ordered stream: commands per chunk cap (0 = default: with the 8-byte
+ *                           table min(2^pb - 1, 2^27 / k) rounded down to 128, else 2^26 / k)
+ *   "wide_subchunk"         add / contains on a filter past 2^32 bits: keys per sub-chunk cap (0 =
+ *                           default 2^29 / k, which bounds the first-setter table at 2^30 entries)
  *   "stream_qgrid"          ordered-stream slot contains kernel grid, 256..8192 (default 1024)
  *   "stream_table_scale"    ordered stream, 8-byte table entries x 1 (default), 2 or 4
  *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-

@@ -201,6 +201,7 @@ SIGNATURES = {
     "rbx_hll_unpack_max_registers": (C.c_int, [vp, C.POINTER(vp), C.c_uint32, vp, vp]),
     "rbx_bench_gather": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, vp]),
     "rbx_tune": (C.c_int, [C.c_char_p, C.c_int]),
+    "rbx_bench_stream_geometry": (C.c_int, [vp, u64p]),
     "rbx_bench_gather_regions": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint, vp, vp]),
     # include/rbx_selftest.h
     "rbx_selftest_mod": (C.c_uint64, [C.c_uint64, C.c_uint64]),

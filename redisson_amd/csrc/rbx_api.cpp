@@ -190,6 +190,7 @@ struct rbx_ctx {
     DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
     DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
     uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
+    uint64_t st_geom[4] = {0, 0, 0, 0};             // last stream call: bb, fbits, pb, chunk
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
     uint32_t filt_nfids = 0;     // distinct table ids of filt_table
     uint64_t filt_maxbits = 0;   // the largest of their bitmaps, in bits
@@ -1045,6 +1046,8 @@ extern "C" {
 // that leaves the key alone while every other command of the batch runs; the call then fails with
 // RBX_E_REDIS (RedisException) -- an add has set every in-range bit.  Without such an index the
 // replies are the in-order ones.  Chunks run in key order (each sees the previous chunks' bits).
+// rbx_tune("wide_subchunk", n): keys per sub-chunk cap (0 = default 2^29 / k; tests split small batches)
+static uint64_t g_wide_subchunk = 0;
 static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t k, Bitmap *bm, uint8_t *out_flags,
                          uint64_t *out_count, bool is_add) {
     RBX_TRY(c->counters.reserve(64));
@@ -1059,18 +1062,30 @@ static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t 
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     RBX_TRY(pipelined_host_batches(c, keys, c->stream, [&](const KeysDev &dk, uint64_t i0) -> int {
-        if (dk.n >= (1ULL << 32)) return fail(RBX_E_ILLEGAL_ARGUMENT, "chunk exceeds 2^32 keys");
-        uint32_t tl = 10;  // table >= 2x the chunk's bit indexes
-        while ((1ULL << tl) < 2 * dk.n * k) ++tl;
-        unsigned long long *table = nullptr;
-        if (is_add) {
-            RBX_TRY(c->wide_table.reserve(8ULL << tl));
-            table = c->wide_table.as<unsigned long long>();
-            HIP_TRY(hipMemsetAsync(table, 0xff, 8ULL << tl, c->stream));
+        // Sub-chunks of <= 2^29 / k keys, run in key order (each sees the previous one's bits), so
+        // the first-setter table (>= 2x the sub-chunk's bit indexes) stays <= 2^30 entries (8 GiB)
+        // and its 32-bit slot mask well-defined however short the keys (a staging
+        // chunk of empty keys is unbounded in count).
+        uint64_t sub = std::max<uint64_t>(1, (1ULL << 29) / k);
+        if (g_wide_subchunk) sub = std::min<uint64_t>(sub, g_wide_subchunk);
+        for (uint64_t j0 = 0; j0 < dk.n; j0 += sub) {
+            KeysDev sk = dk;
+            sk.n = std::min<uint64_t>(sub, dk.n - j0);
+            if (dk.offsets) sk.offsets = dk.offsets + j0;
+            else sk.bytes = dk.bytes + j0 * dk.stride;
+            uint32_t tl = 10;  // table >= 2x the sub-chunk's bit indexes
+            while ((1ULL << tl) < 2 * sk.n * k) ++tl;
+            if (tl > 30) return fail(RBX_E_ILLEGAL_ARGUMENT, "wide-filter table past 2^30 entries");
+            unsigned long long *table = nullptr;
+            if (is_add) {
+                RBX_TRY(c->wide_table.reserve(8ULL << tl));
+                table = c->wide_table.as<unsigned long long>();
+                HIP_TRY(hipMemsetAsync(table, 0xff, 8ULL << tl, c->stream));
+            }
+            launch_bloom_wide(sk, m, k, bm ? bm->d_words : nullptr, bm ? bm->d_len : nullptr, table, tl, is_add,
+                              d_out ? d_out + i0 + j0 : nullptr, d_count, d_oob, c->stream);
+            HIP_TRY(hipGetLastError());
         }
-        launch_bloom_wide(dk, m, k, bm ? bm->d_words : nullptr, bm ? bm->d_len : nullptr, table, tl, is_add,
-                          d_out ? d_out + i0 : nullptr, d_count, d_oob, c->stream);
-        HIP_TRY(hipGetLastError());
         return RBX_OK;
     }));
     int rc;
@@ -1652,6 +1667,10 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     // chunk bases on 128-command boundaries keep the replies' range images line-aligned
     if (chunk < keys.n && chunk > 128) chunk &= ~127ULL;
     if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
+    c->st_geom[0] = bb;
+    c->st_geom[1] = fbits;
+    c->st_geom[2] = t8 ? pb : 0;
+    c->st_geom[3] = chunk;
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_adds.reserve(chunk * 4));
     const uint32_t pbits = g_stream_prefilter ? (uint32_t)g_stream_prefilter : 20u;
@@ -1674,6 +1693,16 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             c->st_flag_bytes = chunk;
         }
     }
+    // The 8-byte table and the owner flags are cleared only when they grow: every chunk's walk and
+    // final pass restore EMPTY / 0.  A launch or memset failing inside the loop breaks that, so the
+    // guard then marks both as uninitialized and the next call clears them again.
+    struct ResetOnError {
+        rbx_ctx *c;
+        bool ok = false;
+        ~ResetOnError() {
+            if (!ok) c->st_t8_entries = c->st_flag_bytes = 0;
+        }
+    } guard{c};
     for (uint64_t base = 0; base < keys.n; base += chunk) {
         const uint64_t nch = std::min<uint64_t>(chunk, keys.n - base);
         if (!t8) RBX_TRY(ensure_table(c, nch * k, st));
@@ -1717,6 +1746,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
         launch_stream_chunk(s, fl, st);
         HIP_TRY(hipGetLastError());
     }
+    guard.ok = true;
     return RBX_OK;
 }
 
@@ -3125,6 +3155,13 @@ int rbx_enable_peer_access(int device, int peer) {
 }
 
 // Tuning knobs (process-wide).  "contains_stage1": early-exit width of contains (0 = off).
+int rbx_bench_stream_geometry(rbx_ctx *c, uint64_t *out) {
+    if (!c || !out) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->ks.mu);
+    for (int i = 0; i < 4; ++i) out[i] = c->st_geom[i];
+    return RBX_OK;
+}
+
 int rbx_tune(const char *key, int value) {
     if (!key) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL key");
     if (!strcmp(key, "contains_partition")) {
@@ -3181,6 +3218,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "stream_chunk")) {
         if (value < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_chunk >= 0 (0: 2^26 / k commands)");
         g_stream_chunk = (uint64_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "wide_subchunk")) {
+        if (value < 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "wide_subchunk >= 0 (0: 2^29 / k keys)");
+        g_wide_subchunk = (uint64_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_table_scale")) {

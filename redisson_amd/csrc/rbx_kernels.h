@@ -223,9 +223,9 @@ void set_contains_stage1(int v);
 void set_contains_qshape(int v);  // slot kernel (stage 5): P * 10 + Q
 void set_contains_qgrid(int v);
 void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kernel
-void set_stream_contains_lds(int v);
+void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
 void set_stream_probe_batch(int v);
-void set_stream_qgrid(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
+void set_stream_qgrid(int v);  // slot stream-contains kernel grid (blocks)
 int get_contains_stage1();
 
 // hll_kernels.hip

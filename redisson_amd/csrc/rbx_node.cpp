@@ -99,6 +99,48 @@ class GpuWorkers {
     std::vector<std::unique_ptr<W>> ws_;
 };
 
+// Writer-preferring shared mutex for the replication barrier: std::shared_mutex is
+// glibc's reader-preferring rwlock, so under sustained overlapping batches (shared holders) a
+// replicate / DEL of a replicated name (exclusive) could wait forever.  Here a waiting writer stops
+// new shared holders; the batches already inside drain, the writer runs, then they resume.  No
+// holder takes it twice.
+class ReplBarrier {
+  public:
+    void lock() {
+        std::unique_lock<std::mutex> l(m_);
+        ++writers_waiting_;
+        cv_.wait(l, [&] { return !writer_ && readers_ == 0; });
+        --writers_waiting_;
+        writer_ = true;
+    }
+    void unlock() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            writer_ = false;
+        }
+        cv_.notify_all();
+    }
+    void lock_shared() {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return !writer_ && writers_waiting_ == 0; });
+        ++readers_;
+    }
+    void unlock_shared() {
+        bool last;
+        {
+            std::lock_guard<std::mutex> l(m_);
+            last = --readers_ == 0;
+        }
+        if (last) cv_.notify_all();
+    }
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int readers_ = 0, writers_waiting_ = 0;
+    bool writer_ = false;
+};
+
 struct rbx_node {
     std::vector<rbx_ctx *> ctx;
     std::unique_ptr<GpuWorkers> workers;
@@ -112,7 +154,7 @@ struct rbx_node {
     // kernels are done; replicate(on / off), DEL, and dropping the copies after a failed replicated
     // add hold it exclusively.  So a replica copy never misses an add that ran during the copy, and
     // copies are never deleted under a contains already routed to them.
-    std::shared_mutex repl_mu;
+    ReplBarrier repl_mu;
     // test hook (rbx_node_test_fail_adds): the next fail_adds[g] Bloom adds on GPU g fail
     std::unique_ptr<std::atomic<int>[]> fail_adds;
 };
@@ -299,7 +341,7 @@ static void drop_copies_locked(rbx_node *nd, const std::string &nm) {
 }
 
 static void drop_replicas_after_failure(rbx_node *nd, const std::vector<std::string> &names) {
-    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
+    std::unique_lock<ReplBarrier> ex(nd->repl_mu);
     for (const std::string &nm : names) {
         {
             std::lock_guard<std::mutex> lk(nd->mu);
@@ -320,7 +362,7 @@ int rbx_node_bloom_add(rbx_node *nd, rbx_name name, uint64_t size, uint32_t k, c
     const int home = gpu_of(nd, nm);
     int rc;
     {
-        std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
+        std::shared_lock<ReplBarrier> barrier(nd->repl_mu);
         if (!is_replicated(nd, nm) || nd->ctx.size() == 1)
             return node_add_on(nd, home, name, size, k, keys, out_new, out_count);
         rc = per_gpu(nd, all_gpus(nd), [&](int g) -> int {
@@ -346,7 +388,7 @@ int rbx_node_bloom_contains(rbx_node *nd, rbx_name name, uint64_t size, uint32_t
     const std::string nm = str_of(name);
     const int home = gpu_of(nd, nm);
     const uint64_t N = nd->ctx.size();
-    std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
+    std::shared_lock<ReplBarrier> barrier(nd->repl_mu);
     if (!keys || keys->n < N || !is_replicated(nd, nm) || N == 1)
         return rbx_bloom_contains_n(nd->ctx[home], name, size, k, keys, out_present, out_count);
     if (keys->n && !keys->bytes) return fail(RBX_E_ILLEGAL_ARGUMENT, "keys->bytes is NULL");
@@ -379,7 +421,7 @@ int rbx_node_bloom_replicate(rbx_node *nd, rbx_name name, int on) {
         if (g != home) others.push_back(g);
     // exclusive: no add runs between the copy and the routing change, and no contains still runs on
     // a copy when it is deleted
-    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
+    std::unique_lock<ReplBarrier> ex(nd->repl_mu);
     if (on) {
         rbx_bloom_config cfg;
         NODE_TRY(rbx_bloom_read_config_n(nd->ctx[home], name, &cfg));  // not initialized: ISE
@@ -458,8 +500,23 @@ static std::vector<std::string> filters_of(const std::string &key) {
 int rbx_node_del(rbx_node *nd, const rbx_name *names, uint32_t n, int *deleted) {
     if (!nd || (n && !names)) return fail(RBX_E_ILLEGAL_ARGUMENT, "NULL argument");
     for (uint32_t i = 0; i < n; ++i) NODE_TRY(check_name(names[i]));
-    // exclusive: no batch still runs on a copy being deleted
-    std::unique_lock<std::shared_mutex> ex(nd->repl_mu);
+    // Exclusive only when a name (or the filter of a config name) is replicated: then no batch may
+    // still run on a copy being deleted.  Otherwise the barrier is held shared, like a batch's, so a
+    // DEL of plain names neither waits for the node's in-flight batches nor blocks new ones (ADVICE
+    // r04); holding it shared also keeps a replicate() of these names from starting meanwhile.
+    std::shared_lock<ReplBarrier> sh(nd->repl_mu);
+    bool any = false;
+    {
+        std::lock_guard<std::mutex> lk(nd->mu);
+        if (!nd->replicated.empty())
+            for (uint32_t i = 0; i < n && !any; ++i)
+                for (const std::string &f : filters_of(str_of(names[i]))) any = any || nd->replicated.count(f) != 0;
+    }
+    std::unique_lock<ReplBarrier> ex;
+    if (any) {  // (the names are re-checked below under nd->mu, one by one)
+        sh.unlock();
+        ex = std::unique_lock<ReplBarrier>(nd->repl_mu);
+    }
     std::vector<std::vector<rbx_name>> by(nd->ctx.size());
     std::vector<std::vector<rbx_name>> replica_keys(nd->ctx.size());  // copies: not counted
     std::deque<std::string> held;  // names the replica deletions add (a config's filter bitmap)
@@ -635,7 +692,7 @@ static int bloom_multi(rbx_node *nd, const rbx_name *names, uint32_t nseg, const
     std::vector<std::string> unreplicated;  // replicated names of a failed add
     int rc;
     {
-        std::shared_lock<std::shared_mutex> barrier(nd->repl_mu);
+        std::shared_lock<ReplBarrier> barrier(nd->repl_mu);
         {
             std::lock_guard<std::mutex> lk(nd->mu);
             if (!nd->replicated.empty())

@@ -32,13 +32,17 @@ def _zipf_tenants(rng, nt, n, s=1.0):
 
 
 def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
-             occupancy=None, probe_batch=None, table_scale=None):
+             occupancy=None, probe_batch=None, table_scale=None, hot_last=False, geometry=None):
+    """expected: one tryInit size for every tenant, or a per-tenant list.  hot_last: the Zipf-hottest
+    tenant is the LAST handle (the largest filter id of the call) instead of the first.  geometry:
+    the (bb, fbits, pb, chunk) the call must have run with (rbx_bench_stream_geometry)."""
     rng = np.random.default_rng(seed)
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs, handles = [], []
-    for nm in names:
+    sizes = [expected] * nt if np.isscalar(expected) else list(expected)
+    for nm, ex in zip(names, sizes):
         f = client.getBloomFilter(nm)
-        assert f.tryInit(expected, fpp)
+        assert f.tryInit(ex, fpp)
         nb = (f.getSize() + 7) // 8
         bm = rng.integers(0, 256, size=nb, dtype=np.uint8)  # design fill 0.5
         f.importBitmap(bm.tobytes())
@@ -48,6 +52,9 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         refs.append(r)
         handles.append(BloomHandle(client, nm))
     kf = _zipf_tenants(rng, nt, n)
+    if hot_last:
+        first, last = kf == 0, kf == nt - 1
+        kf[first], kf[last] = nt - 1, 0
     if nt > 1 << 16:  # ids past 2^16 (the tag's filter-id field, the prefilter hash) really occur
         assert int(kf.max()) >= 1 << 16 and np.count_nonzero(kf >= 1 << 8) > n // 4
     op = (rng.random(n) < 0.1).astype(np.uint8)
@@ -73,6 +80,10 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_table_scale", table_scale) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
+        if geometry is not None:
+            g = np.zeros(4, np.uint64)
+            assert L.lib().rbx_bench_stream_geometry(client.ctx, g.ctypes.data_as(L.u64p)) == 0
+            assert tuple(int(x) for x in g) == tuple(geometry), (g, geometry)
     finally:
         L.lib().rbx_tune(b"stream_chunk", 0)
         L.lib().rbx_tune(b"stream_contains_slots", STREAM_SLOTS_DEFAULT)
@@ -221,3 +232,21 @@ def test_stream_k20_variable_keys(client, fresh, table8):
         h.close()
     for nm in names:
         client.getBloomFilter(nm).delete()
+
+
+def test_c5_production_entry_packing(client, fresh):
+    """the bench leg's own 8-byte entry packing, ((fid << bb | bit) << pb) | position
+    with bb = 24 (a 14,377,587-bit tenant), fbits = 17 (100,000 filter ids) and pb = 23, and the
+    production chunk: min(2^23 - 1, 2^27 / 10) rounded down to 128 = 8,388,480 commands, with no
+    stream_chunk override.  9.2M commands = one full chunk + a second one, so positions run to the
+    top of the 23-bit field.  99,999 tryInit(1000, 1e-3) tenants (14,377 bits) + one tryInit(1e6,
+    1e-3) tenant, all k = 10 (k_stream_*<64, 16>); the big tenant is the Zipf-hottest AND the last
+    handle (filter id 99,999 >= 2^16), so its claims fill every field at once.  Replies, counts and
+    all 100,000 bitmaps vs the oracle (M/RedissonBloomFilter.java:99-102,198-201)."""
+    nt = 100_000
+    sizes = [1000] * (nt - 1) + [1_000_000]
+    chunk = ((1 << 23) - 1) & ~127
+    assert chunk == 8_388_480 and chunk < (1 << 27) // 10
+    wc = _c5_case(client, fresh, seed=0xC5B0023, nt=nt, expected=sizes, fpp=1e-3, n=9_200_000, hot_last=True,
+                  geometry=(24, 17, 23, chunk))
+    assert wc[1] > 100_000

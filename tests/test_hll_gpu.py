@@ -553,3 +553,73 @@ def test_sparse_set_string_past_the_slot_copies(client, fresh):
         assert s[4] == 1 and s == ref.string(s[8:16])
         g.delete()
     client.getHyperLogLog(fresh).delete()
+
+
+def test_c4_10k_hlls_three_pool_chunks(client, fresh):
+    """config C4 at its HLL count.  10,000 HLLs in ONE multi-key PFADD batch
+    (M/RedissonHyperLogLog.java:76-102 addAll per key, pipelined): the register pool holds 4,096
+    HLLs per 64 MiB chunk, so the batch spans three chunks.  200..2,400 16-byte elements per key
+    (some keys stay sparse, the larger ones promote to dense mid-command).  Checked against the
+    oracle: every PFADD reply, every key's PFCOUNT, the GET bytes (sparse or dense as Redis holds
+    them) of 150 keys sampled from all three chunks; then pack_registers over all 10,000 (sampled
+    rows vs the oracle's registers) and unpack_max of a random register image (every count and
+    sampled registers vs max(oracle, image))."""
+    import ctypes as C
+
+    import torch
+
+    from redisson_amd import _lib as L
+
+    rng = np.random.default_rng(0xC4C4)
+    nk = 10_000
+    keys = [f"{fresh}-{i}" for i in range(nk)]
+    per = rng.integers(200, 2401, size=nk)
+    segs = np.zeros(nk + 1, np.uint64)
+    segs[1:] = np.cumsum(per)
+    mat = rng.integers(0, 256, size=(int(segs[-1]), 16), dtype=np.uint8)
+    replies = hll_add_multi(client, keys, segs, Arena.fixed(mat))
+    refs = [O.RedisHll() for _ in keys]
+    for i in range(nk):
+        ch = refs[i].pfadd(*O.fixed_arena(mat[int(segs[i]):int(segs[i + 1])]))
+        assert bool(replies[i]) == bool(ch), i
+    counts = hll_count_each(client, keys)
+    want = np.array([O.hll_count(r.regs) for r in refs], np.uint64)
+    assert np.array_equal(np.asarray(counts, np.uint64), want)
+    dense = sum(int(r.dense.value) for r in refs)
+    assert 0 < dense < nk  # both encodings occur
+    sample = sorted(set(rng.choice(nk, size=147, replace=False).tolist()) | {0, 4095, 4096, 8191, 8192, nk - 1})
+    assert any(i < 4096 for i in sample) and any(4096 <= i < 8192 for i in sample) and any(i >= 8192 for i in sample)
+    for i in sample:
+        s = client.getHyperLogLog(keys[i]).exportString()
+        assert s == refs[i].string(s[8:16]), i
+
+    hs = []
+    for nm in keys:
+        hp = C.c_void_p()
+        assert L.lib().rbx_hll_open(client.ctx, nm.encode(), 0, C.byref(hp)) == 0
+        hs.append(hp.value)
+    arr = (C.c_void_p * nk)(*hs)
+    try:
+        buf = torch.zeros(nk * 16384, dtype=torch.uint8, device="cuda")
+        assert L.lib().rbx_hll_pack_registers(client.ctx, arr, nk, buf.data_ptr(), None) == 0
+        L.lib().rbx_synchronize(client.ctx)
+        got = buf.view(nk, 16384)
+        for i in sample:
+            assert np.array_equal(got[i].cpu().numpy(), refs[i].regs), i
+        other = torch.randint(0, 4, (nk, 16384), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        assert L.lib().rbx_hll_unpack_max_registers(client.ctx, arr, nk, other.data_ptr(), None) == 0
+        out = np.zeros(nk, np.uint64)
+        assert L.lib().rbx_hll_count_each_handles(client.ctx, arr, nk, out.ctypes.data_as(L.u64p)) == 0
+        oth = other.cpu().numpy()
+        mx = np.maximum(np.stack([r.regs for r in refs]), oth)
+        want2 = np.array([O.hll_count(mx[i]) for i in range(nk)], np.uint64)
+        assert np.array_equal(out, want2)
+        for i in sample:
+            d = client.getHyperLogLog(keys[i]).exportDense()
+            assert np.array_equal(O.hll_dense_unpack(d[16:]), mx[i]), i
+    finally:
+        for h in hs:
+            L.lib().rbx_hll_close(h)
+    for nm in keys:
+        client.getHyperLogLog(nm).delete()

@@ -212,6 +212,29 @@ def test_filter_just_past_2_32_bits(client, fresh):
     f.delete()
 
 
+def test_wide_filter_short_keys_in_subchunks(client, fresh):
+    """a staging chunk of empty / 1-byte keys holds any number of keys, so the wide
+    path splits it into sub-chunks (<= 2^29 / k keys: a first-setter table of <= 2^30 entries).
+    Here the sub-chunk is capped at 7,001 keys (rbx_tune wide_subchunk) so one 60K-key batch of
+    empty, 1- and 2-byte keys (massively repeated: the same bits recur across sub-chunks) runs in
+    nine sub-chunks in key order; per-key flags, counts and the bitmap vs the oracle."""
+    f = client.getBloomFilter(fresh)
+    assert f.tryInit(-448_089_843, 0.01)
+    size, k = f.getSize(), f.getHashIterations()
+    ref = O.OracleBloom(size, k)
+    rng = np.random.default_rng(33)
+    pool = [b""] + [bytes([i]) for i in range(256)] + [rng.bytes(2) for _ in range(300)]
+    batch = [pool[int(j)] for j in rng.integers(0, len(pool), size=60_000)]
+    assert L.lib().rbx_tune(b"wide_subchunk", 7001) == 0
+    try:
+        assert _wide_call(f, ref, batch, True)
+        assert _wide_call(f, ref, batch[:30_000] + [rng.bytes(3) for _ in range(30_000)], False)
+    finally:
+        L.lib().rbx_tune(b"wide_subchunk", 0)
+    assert f.exportBitmap() == ref.redis_string()
+    f.delete()
+
+
 def test_binary_bloom_names(client, fresh):
     rng = np.random.default_rng(24)
     n1, n2 = fresh.encode() + b"\x00x", fresh.encode() + b"\x00y"
