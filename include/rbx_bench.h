@@ -79,6 +79,9 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *   "stream_table_scale"    ordered stream, 8-byte table entries x 1 (default), 2 or 4
  *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-
  *                           slot CAS) all in flight at once, 0 one after another
+ *   "stream_diag"           DIAGNOSTICS ONLY, answers become wrong (timing A/Bs): bits 1 = stream
+ *                           contains skip the first-setter lookups, 2 = walk ORs with plain stores,
+ *                           4 = walk writes no owner flags, 8 = probe makes no claims
  *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
  *                           resident blocks (default 33000: four per CU; 0: registers decide)
  *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,

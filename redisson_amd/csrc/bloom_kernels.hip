@@ -789,7 +789,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                                                            unsigned long long *__restrict__ counts,
                                                            const unsigned long long *__restrict__ T8, uint32_t bb,
                                                            uint32_t pb, uint32_t kmax,
-                                                           const uint32_t *__restrict__ nadds) {
+                                                           const uint32_t *__restrict__ nadds, uint32_t diag = 0) {
     constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
     const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
     struct alignas(16) QEnt {
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
             bool fin_p = false;
             if (act[s]) {
                 bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
-                if (clear) {  // set by an earlier add of this chunk?  Only if the filter says so.
+                if (clear && !(diag & 1)) {  // set by an earlier add of this chunk?  Only if the filter says so.
                     if (maybe_claimed(prefilter, pshift, sfid[s], sidx[s], ((uint64_t)sfid[s] << bb) | sidx[s], lg8))
                         clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
                                       : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
@@ -1004,6 +1004,7 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
+        if (batch == 2) zm = 0;  // DIAGNOSTIC: no claims
         if (batch) {
             const uint64_t mask = (1ULL << lg) - 1;
             unsigned long long old[KMAX];
@@ -1066,7 +1067,8 @@ __global__ __launch_bounds__(256) void k_stream_occ(const unsigned long long *__
 // every entry: OR its bit into its bitmap, flag its owner, empty the slot (two entries per lane)
 __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restrict__ T, const uint32_t *__restrict__ nadds,
                                                      uint32_t kmax, uint32_t bb, uint32_t pb,
-                                                     uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag) {
+                                                     uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag,
+                                                     uint32_t diag = 0) {
     const uint32_t lg = t8_log2(*nadds, kmax);
     const uint64_t n2 = (1ULL << lg) / 2;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1081,8 +1083,9 @@ __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restr
             if (v == ~0ULL) continue;
             const uint64_t key = v >> pb;
             const uint32_t bit = (uint32_t)(key & bmask);
-            atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
-            flag[v & pmask] = 1;
+            if (diag & 2) fid_bm[key >> bb][bit >> 5] |= bit_in_word(bit);  // DIAGNOSTIC (racy)
+            else atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
+            if (!(diag & 4)) flag[v & pmask] = 1;
         }
         ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
     }
@@ -1508,6 +1511,11 @@ void set_stream_contains_lds(int v) { g_stream_lds = v; }
 // claim after another (rbx_tune "stream_probe_batch")
 static uint32_t g_probe8_batch = 1;
 void set_stream_probe_batch(int v) { g_probe8_batch = (uint32_t)v; }
+// DIAGNOSTICS ONLY (timing; answers become wrong): 1 = the stream contains skip the first-setter
+// lookups, 2 = the walk ORs bits with plain read-modify-writes, 4 = the walk writes no owner flags,
+// 8 = the probe makes no claims
+static uint32_t g_stream_diag = 0;
+void set_stream_diag(int v) { g_stream_diag = (uint32_t)v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1517,7 +1525,8 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                        a.nadds);
     if (a.t8)
         hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.prefilter, a.pshift, g_probe8_batch);
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.prefilter, a.pshift,
+                           (g_stream_diag & 8) ? 2u : g_probe8_batch);
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
@@ -1526,14 +1535,14 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
                            a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
-                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds);
+                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds, g_stream_diag);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
                            a.t8, a.bb, a.pb, a.tkmax, a.nadds);
     if (a.t8) {
         hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
-                           a.flag);
+                           a.flag, g_stream_diag);
         hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);
     } else {
         hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,

@@ -3256,6 +3256,12 @@ int rbx_tune(const char *key, int value) {
         set_stream_qgrid(value);
         return RBX_OK;
     }
+    // DIAGNOSTICS ONLY (timing; answers become wrong): see set_stream_diag
+    if (!strcmp(key, "stream_diag")) {
+        if (value < 0 || (value & ~15) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_diag: bits of 1|2|4|8");
+        set_stream_diag(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "stream_probe_batch")) {
         if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_probe_batch: 0 or 1");
         set_stream_probe_batch(value);

@@ -225,6 +225,7 @@ void set_contains_qgrid(int v);
 void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kernel
 void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
 void set_stream_probe_batch(int v);
+void set_stream_diag(int v);  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
 void set_stream_qgrid(int v);  // slot stream-contains kernel grid (blocks)
 int get_contains_stage1();
 
