@@ -79,6 +79,11 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *   "stream_table_scale"    ordered stream, 8-byte table entries x 1 (default), 2 or 4
  *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-
  *                           slot CAS) all in flight at once, 0 one after another
+ *   "stream_owner"          ordered stream, 8-byte table: 1 (default) add replies from the slot of each
+ *                           add's first zero-bit claim (k_stream_final8, before the walk), 0 owner flags
+ *                           written by the walk (r04)
+ *   "stream_lookup_rounds"  ordered-stream slot contains, 8-byte table, no prefilter: 1 (default) a
+ *                           first-setter lookup is a round of its slot, 0 looked up inline
  *   "stream_diag"           DIAGNOSTICS ONLY, answers become wrong (timing A/Bs): bits 1 = stream
  *                           contains skip the first-setter lookups, 2 = walk ORs with plain stores,
  *                           4 = walk writes no owner flags, 8 = probe makes no claims

@@ -581,20 +581,22 @@ __device__ __forceinline__ uint64_t t8_slot(uint64_t key, uint32_t lg) {
     return ((key + 1) * 0x9E3779B97F4A7C15ULL) >> (64 - lg);
 }
 
-__device__ __forceinline__ void t8_insert(unsigned long long *__restrict__ T, uint32_t lg, uint32_t pb, uint64_t key,
-                                          uint32_t pos) {
+// returns the slot that holds key's entry
+__device__ __forceinline__ uint32_t t8_insert(unsigned long long *__restrict__ T, uint32_t lg, uint32_t pb, uint64_t key,
+                                              uint32_t pos) {
     const uint64_t mask = (1ULL << lg) - 1;
     const unsigned long long mine = ((unsigned long long)key << pb) | pos;
     uint64_t slot = t8_slot(key, lg);
     for (uint64_t probes = 0; probes <= mask; ++probes) {
         const unsigned long long old = atomicCAS(&T[slot], ~0ULL, mine);
-        if (old == ~0ULL) return;
+        if (old == ~0ULL) return (uint32_t)slot;
         if ((old >> pb) == key) {
             if (old > mine) atomicMin(&T[slot], mine);
-            return;
+            return (uint32_t)slot;
         }
         slot = (slot + 1) & mask;
     }
+    return (uint32_t)slot;
 }
 
 // the first setter's chunk position of key, ~0u when no add of the chunk meets it at 0
@@ -789,9 +791,16 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                                                            unsigned long long *__restrict__ counts,
                                                            const unsigned long long *__restrict__ T8, uint32_t bb,
                                                            uint32_t pb, uint32_t kmax,
-                                                           const uint32_t *__restrict__ nadds, uint32_t diag = 0) {
+                                                           const uint32_t *__restrict__ nadds, uint32_t diag = 0,
+                                                           uint32_t lookup_rounds = 0) {
     constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
     const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
+    // r05: with the 8-byte table and no prefilter, a clear bit's first-setter lookup is a round of
+    // its own: the slot's next load is the table entry instead of a bitmap word, in flight with
+    // the other slots' gathers (inline, each lookup chain stalled the lane's whole round)
+    const bool rounds = lookup_rounds && T8 && !prefilter && !(diag & 1);
+    const uint32_t tmask = (uint32_t)((1ULL << lg8) - 1);
+    const uint64_t pmask = (1ULL << pb) - 1;
     struct alignas(16) QEnt {
         uint64_t h1, h2;
         uint32_t t, fi, idx0, pad;  // chunk-local command index, filter index, first bit
@@ -827,13 +836,13 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
         }
         __builtin_amdgcn_wave_barrier();
     };
-    bool act[P];
+    bool act[P], sph[P];  // sph: the slot's next load is a first-setter table entry (lookup round)
     uint64_t sh1[P], sh2[P], sh[P];
-    uint32_t st[P], sjk[P], sidx[P], sfid[P];  // command index, j | k << 16, bit index, table id
+    uint32_t st[P], sjk[P], sidx[P], sfid[P], tsl[P];  // command index, j | k << 16, bit index, table id, table slot
     const uint32_t *sbm[P];
     ModC smp[P];
 #pragma unroll
-    for (int s = 0; s < P; ++s) act[s] = false;
+    for (int s = 0; s < P; ++s) act[s] = sph[s] = false;
     uint32_t cur = 0, qpos = 0;
     int stale = -1;
     fill(0);
@@ -882,10 +891,12 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
 #pragma unroll
         for (int s = 0; s < P; ++s) any |= act[s];
         if (!__ballot(any)) break;
-        uint32_t w[P];
+        unsigned long long e8[P];  // a table entry (lookup round) or, in its low half, a bitmap word
 #pragma unroll
-        for (int s = 0; s < P; ++s)
-            if (act[s]) w[s] = sbm[s][sidx[s] >> 5];
+        for (int s = 0; s < P; ++s) {
+            if (act[s] && sph[s]) e8[s] = T8[tsl[s]];
+            else if (act[s]) e8[s] = sbm[s][sidx[s] >> 5];
+        }
         if (stale >= 0) {
             fill((uint32_t)stale);
             stale = -1;
@@ -894,11 +905,28 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
         for (int s = 0; s < P; ++s) {
             bool fin_p = false;
             if (act[s]) {
-                bool clear = (w[s] & bit_in_word(sidx[s])) == 0u;
-                if (clear && !(diag & 1)) {  // set by an earlier add of this chunk?  Only if the filter says so.
-                    if (maybe_claimed(prefilter, pshift, sfid[s], sidx[s], ((uint64_t)sfid[s] << bb) | sidx[s], lg8))
-                        clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
-                                      : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
+                bool clear;
+                if (sph[s]) {  // lookup round: EMPTY ends the probe (not claimed), another key probes on
+                    const uint64_t key = ((uint64_t)sfid[s] << bb) | sidx[s];
+                    const unsigned long long e = e8[s];
+                    if (e != ~0ULL && (e >> pb) != key) {
+                        tsl[s] = (tsl[s] + 1) & tmask;
+                        continue;
+                    }
+                    sph[s] = false;
+                    clear = e == ~0ULL || !((uint32_t)(e & pmask) < st[s]);
+                } else {
+                    clear = ((uint32_t)e8[s] & bit_in_word(sidx[s])) == 0u;
+                    if (clear && rounds) {
+                        sph[s] = true;
+                        tsl[s] = (uint32_t)t8_slot(((uint64_t)sfid[s] << bb) | sidx[s], lg8);
+                        continue;
+                    }
+                    if (clear && !(diag & 1)) {  // set by an earlier add of this chunk?  Only if the filter says so.
+                        if (maybe_claimed(prefilter, pshift, sfid[s], sidx[s], ((uint64_t)sfid[s] << bb) | sidx[s], lg8))
+                            clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
+                                          : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
+                    }
                 }
                 bool fin = clear;
                 if (!clear && ((++sjk[s]) & 0xffffu) >= (sjk[s] >> 16)) {
@@ -974,7 +1002,8 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
                                                        const uint32_t *__restrict__ kf, unsigned long long *__restrict__ T,
                                                        uint32_t bb, uint32_t pb, uint32_t kmax,
                                                        uint32_t *__restrict__ prefilter, uint32_t pshift,
-                                                       uint32_t batch) {
+                                                       uint32_t batch, uint32_t *__restrict__ zmask,
+                                                       uint32_t *__restrict__ fslot) {
     const uint32_t na = *nadds;
     const uint32_t lg = t8_log2(na, kmax);
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1005,6 +1034,9 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
         for (int j = 0; j < KMAX; ++j)
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
         if (batch == 2) zm = 0;  // DIAGNOSTIC: no claims
+        // the slot of the first zero bit's entry: k_stream_final8 decides the reply from it
+        const uint32_t j0 = zm ? (uint32_t)(__ffs(zm) - 1) : 0u;
+        uint32_t fs = 0;
         if (batch) {
             const uint64_t mask = (1ULL << lg) - 1;
             unsigned long long old[KMAX];
@@ -1017,7 +1049,7 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
             }
 #pragma unroll
             for (int j = 0; j < KMAX; ++j) {
-                if (!(zm & (1u << j)) || old[j] == ~0ULL) continue;
+                if (!(zm & (1u << j))) continue;
                 const uint64_t key = ((uint64_t)f.fid << bb) | idxs[j];
                 const unsigned long long mine = ((unsigned long long)key << pb) | t;
                 uint64_t slot = t8_slot(key, lg);
@@ -1031,11 +1063,19 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
                     slot = (slot + 1) & mask;
                     o = atomicCAS(&T[slot], ~0ULL, mine);
                 }
+                if ((uint32_t)j == j0) fs = (uint32_t)slot;
             }
         } else {
 #pragma unroll
             for (int j = 0; j < KMAX; ++j)
-                if (zm & (1u << j)) t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
+                if (zm & (1u << j)) {
+                    const uint32_t sl = t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
+                    if ((uint32_t)j == j0) fs = sl;
+                }
+        }
+        if (zmask) {
+            zmask[a] = zm;
+            fslot[a] = fs;
         }
         if (prefilter && pshift) {  // pshift 0: occupancy bitmap, built by k_stream_occ
 #pragma unroll
@@ -1085,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restr
             const uint32_t bit = (uint32_t)(key & bmask);
             if (diag & 2) fid_bm[key >> bb][bit >> 5] |= bit_in_word(bit);  // DIAGNOSTIC (racy)
             else atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
-            if (!(diag & 4)) flag[v & pmask] = 1;
+            if (flag && !(diag & 4)) flag[v & pmask] = 1;
         }
         ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
     }
@@ -1104,6 +1144,56 @@ __global__ __launch_bounds__(256) void k_stream_final(uint64_t base, const uint3
         if (v) flag[t] = 0;
         if (out) out[base + t] = v;
         added += v;
+    }
+    if (counts) block_add_u64(added, counts + 1);
+}
+
+// r05: replies and the new-add count without owner flags, BEFORE the walk empties the table.  An
+// add is new iff it is the first setter of one of its zero bits; the entry of its FIRST zero bit
+// (slot recorded by the probe) decides almost every add at one load: position == t -> new.  Only when
+// an earlier add of the chunk claimed that bit too (a shared bit: the same key added twice, or two
+// keys colliding on a bit) are the remaining zero bits looked up, the indexes recomputed from the key.
+// (The r04 walk stored a flag byte per owned bit -- ~4.3 per add, scattered -- and a final pass read
+// them back.)
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_stream_final8(KeysDev keys, uint64_t base, const uint32_t *__restrict__ adds,
+                                                       const uint32_t *__restrict__ nadds,
+                                                       const FilterDesc *__restrict__ filt,
+                                                       const uint32_t *__restrict__ kf,
+                                                       const unsigned long long *__restrict__ T, uint32_t bb,
+                                                       uint32_t pb, uint32_t kmax, const uint32_t *__restrict__ zmask,
+                                                       const uint32_t *__restrict__ fslot, uint8_t *__restrict__ out,
+                                                       unsigned long long *__restrict__ counts) {
+    uint64_t added = 0;
+    const uint32_t na = *nadds;
+    const uint32_t lg = t8_log2(na, kmax);
+    const uint64_t pmask = (1ULL << pb) - 1;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
+        const uint32_t t = adds[a];
+        const uint32_t zm = zmask[a];
+        bool isnew = false;
+        if (zm) {
+            isnew = (T[fslot[a]] & pmask) == t;
+            const uint32_t rest = zm & (zm - 1);
+            if (!isnew && rest) {  // the first zero bit is shared with an earlier add: the others
+                const uint64_t i = base + t;
+                const FilterDesc f = filt[kf[i]];
+                uint64_t h1, h2;
+                hash_key<KLEN>(keys, i, h1, h2);
+                uint64_t h = h1;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (((rest >> j) & 1u) && !isnew) {
+                        const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                        isnew = t8_find(T, lg, pb, ((uint64_t)f.fid << bb) | idx) == t;
+                    }
+                    h += (j & 1) ? h1 : h2;
+                }
+            }
+        }
+        if (out) out[base + t] = isnew;
+        added += isnew;
     }
     if (counts) block_add_u64(added, counts + 1);
 }
@@ -1516,6 +1606,14 @@ void set_stream_probe_batch(int v) { g_probe8_batch = (uint32_t)v; }
 // 8 = the probe makes no claims
 static uint32_t g_stream_diag = 0;
 void set_stream_diag(int v) { g_stream_diag = (uint32_t)v; }
+// r05 (rbx_tune "stream_owner"): 1 (default) replies from the first claims' slots (k_stream_final8),
+// 0 the r04 owner flags written by the walk (k_stream_final)
+static int g_stream_owner = 1;
+void set_stream_owner(int v) { g_stream_owner = v; }
+// r05 (rbx_tune "stream_lookup_rounds"): 1 (default) the slot contains kernel issues a first-setter
+// lookup as one more round of its slot (in flight with the other slots' gathers), 0 inline
+static uint32_t g_stream_lookup_rounds = 1;
+void set_stream_lookup_rounds(int v) { g_stream_lookup_rounds = (uint32_t)v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1523,10 +1621,12 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned cgrid = (unsigned)((a.nchunk + 4095) / 4096);
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
+    const bool own8 = a.t8 && g_stream_owner == 1;  // r05: replies from the first claims, no flags
     if (a.t8)
         hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.prefilter, a.pshift,
-                           (g_stream_diag & 8) ? 2u : g_probe8_batch);
+                           (g_stream_diag & 8) ? 2u : g_probe8_batch, own8 ? a.zmask : nullptr,
+                           own8 ? a.fslot : nullptr);
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
@@ -1535,12 +1635,18 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     if (g_stream_slots)
         hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
                            a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
-                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds, g_stream_diag);
+                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds, g_stream_diag,
+                           g_stream_lookup_rounds);
     else
         hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
                            a.t8, a.bb, a.pb, a.tkmax, a.nadds);
-    if (a.t8) {
+    if (own8) {
+        hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.zmask, a.fslot, a.out, a.counts);
+        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
+                           (uint8_t *)nullptr, g_stream_diag);
+    } else if (a.t8) {
         hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
                            a.flag, g_stream_diag);
         hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);

@@ -189,6 +189,7 @@ struct rbx_ctx {
     DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
     DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
     DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
+    DevBuf st_fslot;             // ordered stream (r05): per add, the slot of its first zero bit's claim
     uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
     uint64_t st_geom[4] = {0, 0, 0, 0};             // last stream call: bb, fbits, pb, chunk
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
@@ -889,7 +890,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ}) {
+                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -1673,6 +1674,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     c->st_geom[3] = chunk;
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_adds.reserve(chunk * 4));
+    if (t8) RBX_TRY(c->st_fslot.reserve(chunk * 4));
     const uint32_t pbits = g_stream_prefilter ? (uint32_t)g_stream_prefilter : 20u;
     const uint64_t kPrefilterWords = 1ULL << (pbits - 5);
     RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
@@ -1714,6 +1716,7 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             s.fid_bm = c->fid_table.as<uint32_t *>();
             s.tkmax = kmax * (uint32_t)g_stream_table_scale;
             s.flag = c->st_flag.as<uint8_t>();
+            s.fslot = c->st_fslot.as<uint32_t>();
         }
         s.adds = c->st_adds.as<uint32_t>();
         s.nadds = c->st_prefilter.as<uint32_t>() + kPrefilterWords;
@@ -3260,6 +3263,16 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "stream_diag")) {
         if (value < 0 || (value & ~15) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_diag: bits of 1|2|4|8");
         set_stream_diag(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_owner")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_owner: 0 or 1");
+        set_stream_owner(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_lookup_rounds")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_lookup_rounds: 0 or 1");
+        set_stream_lookup_rounds(value);
         return RBX_OK;
     }
     if (!strcmp(key, "stream_probe_batch")) {

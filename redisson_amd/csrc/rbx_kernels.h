@@ -172,7 +172,8 @@ struct StreamChunkArgs {
     uint32_t bb, pb;              // bits of the largest bitmap's bit index / of a chunk position
     uint32_t tkmax;               // sizes the table: 2^t8_log2(*nadds, tkmax), tkmax = kmax x table scale
     uint32_t *const *fid_bm;      // bitmap words per table id (fid)
-    uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks)
+    uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks; stream_owner 0)
+    uint32_t *fslot;              // per add-list entry: the table slot of its first zero bit's claim (r05)
 };
 // entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)
 __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
@@ -225,7 +226,9 @@ void set_contains_qgrid(int v);
 void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kernel
 void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
 void set_stream_probe_batch(int v);
-void set_stream_diag(int v);  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
+void set_stream_diag(int v);
+void set_stream_owner(int v);          // 1 (default) replies from first-claim slots, 0 r04 owner flags
+void set_stream_lookup_rounds(int v);  // 1 (default) slot-kernel lookups as slot rounds, 0 inline  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
 void set_stream_qgrid(int v);  // slot stream-contains kernel grid (blocks)
 int get_contains_stage1();
 

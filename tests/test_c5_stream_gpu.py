@@ -32,7 +32,8 @@ def _zipf_tenants(rng, nt, n, s=1.0):
 
 
 def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
-             occupancy=None, probe_batch=None, table_scale=None, hot_last=False, geometry=None):
+             occupancy=None, probe_batch=None, table_scale=None, hot_last=False, geometry=None, owner=None,
+             lookup_rounds=None):
     """expected: one tryInit size for every tenant, or a per-tenant list.  hot_last: the Zipf-hottest
     tenant is the LAST handle (the largest filter id of the call) instead of the first.  geometry:
     the (bb, fbits, pb, chunk) the call must have run with (rbx_bench_stream_geometry)."""
@@ -78,6 +79,10 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         assert L.lib().rbx_tune(b"stream_probe_batch", probe_batch) == 0
     if table_scale is not None:
         assert L.lib().rbx_tune(b"stream_table_scale", table_scale) == 0
+    if owner is not None:
+        assert L.lib().rbx_tune(b"stream_owner", owner) == 0
+    if lookup_rounds is not None:
+        assert L.lib().rbx_tune(b"stream_lookup_rounds", lookup_rounds) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
         if geometry is not None:
@@ -92,6 +97,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
         L.lib().rbx_tune(b"stream_occupancy", 0)
         L.lib().rbx_tune(b"stream_probe_batch", 1)
         L.lib().rbx_tune(b"stream_table_scale", STREAM_TABLE_SCALE_DEFAULT)
+        L.lib().rbx_tune(b"stream_owner", 1)
+        L.lib().rbx_tune(b"stream_lookup_rounds", 1)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -141,6 +148,20 @@ def test_c5_probe_claims_batched_or_serial(client, fresh, probe_batch):
     common within a chunk, so the atomicMin and the serial probe-on paths both run."""
     _c5_case(client, fresh, seed=616 + probe_batch, nt=120, expected=1_000_000, fpp=1e-3, n=1_400_000,
              chunk=350_000, probe_batch=probe_batch)
+
+
+@pytest.mark.parametrize("owner", [1, 0])
+@pytest.mark.parametrize("lookup_rounds", [1, 0])
+@pytest.mark.parametrize("slots", [1, 0])
+def test_c5_owner_replies_and_lookup_rounds(client, fresh, owner, lookup_rounds, slots):
+    """r05: add replies from the slot of each add's first zero-bit claim (stream_owner 1, default;
+    k_stream_final8 runs before the walk) or from the r04 owner flags (0); first-setter lookups as
+    rounds of the slot kernel (stream_lookup_rounds 1, default) or inline (0); both contains kernels.
+    Keys repeat (a quarter of the stream is distinct) and 80 Zipf tenants share bits within a chunk,
+    so an add's first zero bit is often claimed by an earlier add (final8's slow path) and many
+    contains meet a bit claimed earlier in the chunk (the lookup round finds it)."""
+    _c5_case(client, fresh, seed=929 + 4 * owner + 2 * lookup_rounds + slots, nt=80, expected=1_000_000, fpp=1e-3,
+             n=1_200_000, chunk=400_000, slots=slots, owner=owner, lookup_rounds=lookup_rounds)
 
 
 @pytest.mark.parametrize("scale", [1, 2, 4])
