@@ -69,6 +69,7 @@ def parse():
                    help="C5: step s gives command i key i+s of a pool of n+W+K keys, so every step's (tenant, key) "
                         "pairs are new (1), or replays the same stream each step (0)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline C2 sample time")
+    p.add_argument("--c3-add", type=int, default=1, help="C3 leg: also time the add half (one add_multi per step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-hostpath", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     p.add_argument("--dry-run", action="store_true",
@@ -705,6 +706,7 @@ def run_c3(args, world, rank, local, steps, warmup):
     value = sum_over_ranks(world, n) / step_s
     per_rank_tenants = gather_over_ranks(world, nt)
     present = int(counts.sum().item()) / max(warmup + steps, 1)
+    add = c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, world) if args.c3_add else None
     del pool
     # request roofline at C3's locality: `per` consecutive keys gather inside one 1.8 MB slice
     tbl = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
@@ -736,12 +738,66 @@ def run_c3(args, world, rank, local, steps, warmup):
                      **request_fields(tj, kname, ms, peak, stream_write_peak(client, 1 << 30, stream))},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
+    if add is not None:
+        res["add"] = add
     for h in handles:
         h.close()
     client.shutdown()
     del keys
     torch.cuda.empty_cache()
     return res
+
+
+def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, world):
+    """C3's add half: one multi-tenant add(Collection) per step -- `per` fresh random
+    16-byte keys into each of the rank's tenants (rbx_bloom_add_multi_dev: the 8-byte first-setter
+    table by default).  The key window slides one key per step, so every step's (tenant, key) pairs
+    are new and the adds meet zero bits (~k/2 each at the design fill 0.5)."""
+    import ctypes as C
+
+    import torch
+
+    from redisson_amd import device_keys
+    from redisson_amd import _lib as L
+
+    n = per * nt
+    extra = warmup + steps + 1
+    keys = torch.randint(0, 256, (n + extra, 16), dtype=torch.uint8, device="cuda", generator=g)
+    counts = torch.zeros(nt, dtype=torch.int64, device="cuda")
+    sptr = stream.cuda_stream
+    windows = [device_keys(keys.data_ptr() + 16 * j, n, 16) for j in range(extra)]
+    it = [0]
+
+    def step():
+        dk = windows[it[0] % len(windows)]
+        it[0] += 1
+        assert L.lib().rbx_bloom_add_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
+                                                counts.data_ptr(), sptr) == 0
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    with Timer(stream) as t:
+        for _ in range(steps):
+            step()
+    ms = t.ms / steps
+    step_s = max_over_ranks(world, ms / 1e3)
+    new = int(counts.sum().item()) / max(warmup + steps, 1)
+    # SURVEY 8(d): a key + k x 8 B gathered + k x 8 B RMW
+    algo = n * (16 + 2 * k * 8)
+    tj = args.traffic_json if (args.keys, args.tenants, world) == (100_000_000, 100_000, 1) else None
+    del keys
+    return {"metric": "Bloom add keys/sec (whole node), C3 tenants: one add(Collection) per tenant",
+            "value": sum_over_ranks(world, n) / step_s, "unit": "keys/s", "ms_per_step": step_s * 1e3,
+            "keys_per_gpu": n, "new_keys_per_step": new, "steps": steps, "warmup": warmup,
+            "path": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"
+            if args.tune.find("add_multi_table8=0") < 0 else "16-byte epoch table (k_bloom_add_probe + commit)",
+            "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
+                         "traffic": load_traffic(tj, "madd_pipeline", "hbm_bytes_by_class"),
+                         "requests_per_launch": load_traffic(tj, "madd_pipeline", "requests_per_launch"),
+                         "atomic_requests_per_launch": load_traffic(tj, "madd_pipeline", "atomic_requests_per_launch")}}
 
 
 # ------------------------------------------------------------------------------------------

@@ -613,6 +613,55 @@ __device__ __forceinline__ uint32_t t8_find(const unsigned long long *__restrict
     return 0xffffffffu;
 }
 
+// The zero bits' claims of one add (position t) in the 8-byte table; returns the slot of the first
+// zero bit's entry.  batch: every home-slot CAS in flight at once (a C5 add of the fresh stream meets
+// ~5 zero bits; one CAS round trip after another was a serial chain per lane), then the rare
+// occupied home slot of another bit probes on serially; 0: one insert after another.
+template <int KMAX>
+__device__ __forceinline__ uint32_t t8_claim(unsigned long long *__restrict__ T, uint32_t lg, uint32_t bb, uint32_t pb,
+                                             uint32_t fid, const uint32_t (&idxs)[KMAX], uint32_t zm, uint32_t t,
+                                             uint32_t batch) {
+    const uint32_t j0 = zm ? (uint32_t)(__ffs(zm) - 1) : 0u;
+    uint32_t fs = 0;
+    if (batch) {
+        const uint64_t mask = (1ULL << lg) - 1;
+        unsigned long long old[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (zm & (1u << j)) {
+                const uint64_t key = ((uint64_t)fid << bb) | idxs[j];
+                old[j] = atomicCAS(&T[t8_slot(key, lg)], ~0ULL, ((unsigned long long)key << pb) | t);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (!(zm & (1u << j))) continue;
+            const uint64_t key = ((uint64_t)fid << bb) | idxs[j];
+            const unsigned long long mine = ((unsigned long long)key << pb) | t;
+            uint64_t slot = t8_slot(key, lg);
+            unsigned long long o = old[j];
+            for (uint64_t probes = 0; probes <= mask; ++probes) {
+                if (o == ~0ULL) break;
+                if ((o >> pb) == key) {
+                    if (o > mine) atomicMin(&T[slot], mine);
+                    break;
+                }
+                slot = (slot + 1) & mask;
+                o = atomicCAS(&T[slot], ~0ULL, mine);
+            }
+            if ((uint32_t)j == j0) fs = (uint32_t)slot;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (zm & (1u << j)) {
+                const uint32_t sl = t8_insert(T, lg, pb, ((uint64_t)fid << bb) | idxs[j], t);
+                if ((uint32_t)j == j0) fs = sl;
+            }
+    }
+    return fs;
+}
+
 // ---- ordered mixed stream (C5): key i is a single-key contains (op 0) or add (op 1) on
 // filters[kf[i]], executed in key order.  Per chunk: compact the adds' positions, probe the adds
 // (first-setter table of add positions per initially-zero bit, plus a prefilter bitset of the
@@ -1026,53 +1075,13 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
             }
             h += (j & 1) ? h1 : h2;
         }
-        // the zero bits' claims: every home-slot CAS in flight at once (a C5 add of the fresh stream
-        // meets ~5 zero bits; one CAS round trip after another was a serial chain per lane), then
-        // the rare occupied home slot of another bit probes on serially
         uint32_t zm = 0;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
         if (batch == 2) zm = 0;  // DIAGNOSTIC: no claims
         // the slot of the first zero bit's entry: k_stream_final8 decides the reply from it
-        const uint32_t j0 = zm ? (uint32_t)(__ffs(zm) - 1) : 0u;
-        uint32_t fs = 0;
-        if (batch) {
-            const uint64_t mask = (1ULL << lg) - 1;
-            unsigned long long old[KMAX];
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if (zm & (1u << j)) {
-                    const uint64_t key = ((uint64_t)f.fid << bb) | idxs[j];
-                    old[j] = atomicCAS(&T[t8_slot(key, lg)], ~0ULL, ((unsigned long long)key << pb) | t);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if (!(zm & (1u << j))) continue;
-                const uint64_t key = ((uint64_t)f.fid << bb) | idxs[j];
-                const unsigned long long mine = ((unsigned long long)key << pb) | t;
-                uint64_t slot = t8_slot(key, lg);
-                unsigned long long o = old[j];
-                for (uint64_t probes = 0; probes <= mask; ++probes) {
-                    if (o == ~0ULL) break;
-                    if ((o >> pb) == key) {
-                        if (o > mine) atomicMin(&T[slot], mine);
-                        break;
-                    }
-                    slot = (slot + 1) & mask;
-                    o = atomicCAS(&T[slot], ~0ULL, mine);
-                }
-                if ((uint32_t)j == j0) fs = (uint32_t)slot;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j)
-                if (zm & (1u << j)) {
-                    const uint32_t sl = t8_insert(T, lg, pb, ((uint64_t)f.fid << bb) | idxs[j], t);
-                    if ((uint32_t)j == j0) fs = sl;
-                }
-        }
+        const uint32_t fs = t8_claim<KMAX>(T, lg, bb, pb, f.fid, idxs, zm, t, batch);
         if (zmask) {
             zmask[a] = zm;
             fslot[a] = fs;
@@ -1109,7 +1118,7 @@ __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restr
                                                      uint32_t kmax, uint32_t bb, uint32_t pb,
                                                      uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag,
                                                      uint32_t diag = 0) {
-    const uint32_t lg = t8_log2(*nadds, kmax);
+    const uint32_t lg = nadds ? t8_log2(*nadds, kmax) : kmax;  // no count: kmax carries lg itself
     const uint64_t n2 = (1ULL << lg) / 2;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t pmask = (1ULL << pb) - 1, bmask = (1ULL << bb) - 1;
@@ -1196,6 +1205,97 @@ __global__ __launch_bounds__(256) void k_stream_final8(KeysDev keys, uint64_t ba
         added += isnew;
     }
     if (counts) block_add_u64(added, counts + 1);
+}
+
+// ---- multi-tenant add (r05): the stream's 8-byte first-setter table for add(Collection) batches -
+// A multi-tenant add batch (segment s = keys [seg_off[s], seg_off[s+1]) added to filters[s], the
+// segments in order) is the ordered stream with every command an add: key t of a chunk claims its
+// zero bits with entries ((fid << bb | bit) << pb) | t (one CAS each, t8_claim), the reply comes from
+// the entry of its first zero bit (k_madd_final8), and k_stream_walk ORs every owned bit and empties
+// the table.  The r03 path kept 16-byte epoch-tagged entries (a CAS and an atomicMin per zero bit), a
+// commit that re-hashed every key to look its zero bits up again, and one atomicAdd per new key into
+// its segment's count; here the counts are one atomic per (wave, segment).
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_madd_probe8(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                     const FilterDesc *__restrict__ filt,
+                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                     const uint32_t *__restrict__ tile_seg0,
+                                                     unsigned long long *__restrict__ T, uint32_t lg, uint32_t bb,
+                                                     uint32_t pb, uint32_t batch, uint32_t *__restrict__ zmask,
+                                                     uint32_t *__restrict__ fslot) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint32_t maxidx = 0;
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        uint32_t zm = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
+        const uint32_t fs = t8_claim<KMAX>(T, lg, bb, pb, f.fid, idxs, zm, (uint32_t)t, batch);
+        zmask[t] = zm;
+        fslot[t] = fs;
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_madd_final8(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                     const FilterDesc *__restrict__ filt,
+                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                     const uint32_t *__restrict__ tile_seg0,
+                                                     const unsigned long long *__restrict__ T, uint32_t lg, uint32_t bb,
+                                                     uint32_t pb, const uint32_t *__restrict__ zmask,
+                                                     const uint32_t *__restrict__ fslot, uint8_t *__restrict__ out_new,
+                                                     unsigned long long *__restrict__ seg_counts) {
+    const uint64_t pmask = (1ULL << pb) - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // every lane of a wave runs the same number of iterations (wave_seg_add is a wave operation)
+    const uint64_t n_up = (nchunk + 63) & ~63ULL;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_up; t += stride) {
+        const bool in = t < nchunk;
+        const uint64_t i = base + t;
+        uint32_t seg = 0;
+        bool isnew = false;
+        if (in) {
+            seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
+            const uint32_t zm = zmask[t];
+            if (zm) {
+                isnew = (T[fslot[t]] & pmask) == t;
+                const uint32_t rest = zm & (zm - 1);
+                if (!isnew && rest) {  // the first zero bit is shared with an earlier key: the others
+                    const FilterDesc f = filt[seg];
+                    uint64_t h1, h2;
+                    hash_key<KLEN>(keys, i, h1, h2);
+                    uint64_t h = h1;
+#pragma unroll
+                    for (int j = 0; j < KMAX; ++j) {
+                        if (((rest >> j) & 1u) && !isnew) {
+                            const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                            isnew = t8_find(T, lg, pb, ((uint64_t)f.fid << bb) | idx) == (uint32_t)t;
+                        }
+                        h += (j & 1) ? h1 : h2;
+                    }
+                }
+            }
+            if (out_new) out_new[i] = isnew;
+        }
+        if (seg_counts) wave_seg_add(in, seg, isnew ? 1u : 0u, seg_counts);
+    }
 }
 
 // ---- single-filter fast path: 8-byte entries (bit << 32 | key id), empty = ~0 ------------
@@ -1661,6 +1761,34 @@ static void launch_stream_chunk_len(const StreamChunkArgs &a, hipStream_t st) {
     if (a.kmax <= 8) launch_stream_chunk_k<KLEN, 8>(a, st);
     else if (a.kmax <= 16) launch_stream_chunk_k<KLEN, 16>(a, st);
     else launch_stream_chunk_k<KLEN, 32>(a, st);
+}
+
+template <int KLEN, int KMAX>
+static void launch_madd8_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
+    const unsigned grid = grid_for(a.nchunk, kMaxGrid);
+    hipLaunchKernelGGL((k_madd_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.t8, a.lg, a.bb, a.pb, g_probe8_batch, a.zmask, a.fslot);
+    hipLaunchKernelGGL((k_madd_final8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.t8, a.lg, a.bb, a.pb, a.zmask, a.fslot, a.out_new,
+                       a.seg_counts);
+    hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, (const uint32_t *)nullptr, a.lg, a.bb,
+                       a.pb, a.fid_bm, (uint8_t *)nullptr, 0u);
+}
+
+template <int KLEN>
+static void launch_madd8_chunk_len(const MaddChunkArgs &a, hipStream_t st) {
+    if (a.kmax <= 8) launch_madd8_chunk_k<KLEN, 8>(a, st);
+    else if (a.kmax <= 16) launch_madd8_chunk_k<KLEN, 16>(a, st);
+    else launch_madd8_chunk_k<KLEN, 32>(a, st);
+}
+
+void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st) {
+    switch (klen_fast) {
+    case 16: launch_madd8_chunk_len<16>(a, st); break;
+    case 32: launch_madd8_chunk_len<32>(a, st); break;
+    case 64: launch_madd8_chunk_len<64>(a, st); break;
+    default: launch_madd8_chunk_len<0>(a, st); break;
+    }
 }
 
 void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st) {

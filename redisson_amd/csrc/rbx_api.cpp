@@ -1591,6 +1591,67 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     return RBX_OK;
 }
 
+// rbx_tune("stream_chunk", n) caps a chunk of the ordered stream and of the 8-byte multi-tenant add at
+// n commands (tests: many chunks on small batches).
+static uint64_t g_stream_chunk = 0;
+// rbx_tune("add_multi_table8"): 1 (default) multi-tenant adds on the 8-byte first-setter table
+// (k_madd_*, r05) whenever (filter id, bit) fits 41 bits and k <= 32; 0 the r03 16-byte table path
+static int g_add_multi_t8 = 1;
+
+// Multi-tenant add on the 8-byte table: chunks of <= min(2^pb - 1, 2^27 / k) keys, each probe ->
+// final -> walk, in key order (a chunk's bits are set before the next probes).  The table and its
+// EMPTY state are shared with the ordered stream (st_t8 / st_t8_entries).
+static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg_off, uint32_t nseg,
+                          uint32_t kmax, uint32_t bb, uint32_t pb, uint8_t *d_out_new,
+                          unsigned long long *d_seg_counts, hipStream_t st) {
+    const uint64_t k = std::max<uint32_t>(kmax, 1);
+    const uint64_t cap = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, (1ULL << 27) / k);
+    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, cap));
+    if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
+    const uint32_t lgmax = t8_log2((uint32_t)chunk, (uint32_t)k);
+    const uint64_t entries = 1ULL << lgmax;
+    if (c->st_t8_entries < entries) {
+        c->st_t8_entries = 0;
+        RBX_TRY(c->st_t8.reserve(entries * 8));
+        HIP_TRY(hipMemsetAsync(c->st_t8.p, 0xff, entries * 8, st));
+        c->st_t8_entries = entries;
+    }
+    RBX_TRY(c->zmask.reserve(chunk * 4));
+    RBX_TRY(c->st_fslot.reserve(chunk * 4));
+    struct ResetOnError {  // see rbx_bloom_stream_dev
+        rbx_ctx *c;
+        bool ok = false;
+        ~ResetOnError() {
+            if (!ok) c->st_t8_entries = 0;
+        }
+    } guard{c};
+    const int fl = fast_len(keys);
+    for (uint64_t base = 0; base < keys.n; base += chunk) {
+        MaddChunkArgs a{};
+        a.keys = keys;
+        a.base = base;
+        a.nchunk = std::min<uint64_t>(chunk, keys.n - base);
+        a.filt = c->filt_table.as<FilterDesc>();
+        a.seg_off = d_seg_off;
+        a.nseg = nseg;
+        a.tile_seg0 = c->tile_segs.as<uint32_t>();
+        a.kmax = kmax;
+        a.t8 = c->st_t8.as<unsigned long long>();
+        a.lg = t8_log2((uint32_t)a.nchunk, (uint32_t)k);
+        a.bb = bb;
+        a.pb = pb;
+        a.fid_bm = c->fid_table.as<uint32_t *>();
+        a.zmask = c->zmask.as<uint32_t>();
+        a.fslot = c->st_fslot.as<uint32_t>();
+        a.out_new = d_out_new;
+        a.seg_counts = d_seg_counts;
+        launch_madd8_chunk(a, fl, st);
+        HIP_TRY(hipGetLastError());
+    }
+    guard.ok = true;
+    return RBX_OK;
+}
+
 int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *d_seg_offsets,
                             const rbx_keys *d_keys, uint8_t *d_out_new, unsigned long long *d_counts,
                             void *stream) {
@@ -1606,14 +1667,17 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     KeysDev k = keys_dev(d_keys);
     RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
     launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+    uint32_t bb = 1, fbits = 0;
+    while ((1ULL << bb) < c->filt_maxbits) ++bb;
+    while ((1ULL << fbits) < c->filt_nfids) ++fbits;
+    if (g_add_multi_t8 && kmax <= 32 && bb + fbits <= 41)
+        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st);
     FilterDesc dummy{};
     return run_add(c, k, c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, dummy, kmax, d_out_new, nullptr,
                    d_counts, st);
 }
 
 // Ordered mixed stream (C5): see rbx.h.  Chunks of <= 2^26 pairs run probe -> contains -> commit.
-// rbx_tune("stream_chunk", n) caps a chunk at n commands (tests: many chunks on small streams).
-static uint64_t g_stream_chunk = 0;
 // rbx_tune("stream_prefilter"): pbits in [16, 27] = the adds also set a 2^pbits-bit prefilter that a
 // contains reads before it looks a clear bit up in the first-setter table; 0 (default since r04) =
 // the table alone.  With the 8-byte table (64 MiB for a C5 chunk) a lookup costs less than the
@@ -3263,6 +3327,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "stream_diag")) {
         if (value < 0 || (value & ~15) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_diag: bits of 1|2|4|8");
         set_stream_diag(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_multi_table8")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0 or 1");
+        g_add_multi_t8 = value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_owner")) {

@@ -175,6 +175,24 @@ struct StreamChunkArgs {
     uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks; stream_owner 0)
     uint32_t *fslot;              // per add-list entry: the table slot of its first zero bit's claim (r05)
 };
+// One chunk of a multi-tenant add on the 8-byte first-setter table (r05, bloom_kernels.hip k_madd_*):
+// probe (claims) -> final (replies, per-segment counts) -> walk (OR owned bits, empty the table).
+struct MaddChunkArgs {
+    KeysDev keys;
+    uint64_t base, nchunk;
+    const FilterDesc *filt;
+    const uint64_t *seg_off;
+    uint32_t nseg;
+    const uint32_t *tile_seg0;
+    uint32_t kmax;
+    unsigned long long *t8;   // 2^lg entries, EMPTY before and after the chunk
+    uint32_t lg, bb, pb;
+    uint32_t *const *fid_bm;  // bitmap words per filter id
+    uint32_t *zmask, *fslot;  // per key of the chunk
+    uint8_t *out_new;
+    unsigned long long *seg_counts;
+};
+void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st);
 // entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)
 __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
     const uint64_t need = (uint64_t)nadds * kmax;

@@ -13,6 +13,7 @@ import pytest
 from oracle import oracle as O
 from redisson_amd import (Arena, ArithmeticException, BloomHandle, IllegalArgumentException,
                           IllegalStateException, RedisException, bloom_add_multi, bloom_contains_multi)
+from redisson_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
@@ -329,6 +330,107 @@ def test_multi_tenant_parity(client, fresh):
         h.close()
     for n in names:
         client.getBloomFilter(n).delete()
+
+
+@pytest.mark.parametrize("table8", [1, 0])
+@pytest.mark.parametrize("chunk", [0, 700])
+def test_multi_tenant_add_first_setter_tables(client, fresh, table8, chunk):
+    """r05: multi-tenant add(Collection) on the 8-byte first-setter table (add_multi_table8 1, default:
+    one CAS per zero bit, replies from the first claim's slot, walk commit) and on the r03 16-byte
+    table (0).  Shapes with k up to 17 (KMAX 32), variable-length keys (KLEN 0), repeated tenants
+    and keys repeated inside and across segments (shared bits: the final pass's slow path); chunk
+    700 runs the 8-byte path in many chunks (the in-order fold across chunk boundaries)."""
+    rng = np.random.default_rng(1200 + table8 + chunk)
+    names = [f"{fresh}-{t}" for t in range(6)]
+    shapes = [(14377587, 10), (729, 5), (9585, 7), (64, 7), (1 << 20, 3), (100003, 17)]
+    refs = []
+    for n, (m, k) in zip(names, shapes):
+        client.getBloomFilter(n).tryInitRaw(m, k)
+        refs.append(O.OracleBloom(m, k))
+    handles = [BloomHandle(client, n) for n in names]
+    order = [0, 1, 2, 3, 4, 5, 3, 0, 2, 2]
+    sizes = [int(x) for x in rng.integers(1, 600, size=len(order))]
+    shared = [rng.bytes(int(L)) for L in rng.integers(0, 40, size=50)]
+    keys, segs = [], [0]
+    for t, sz in zip(order, sizes):
+        pool = [rng.bytes(int(L)) for L in rng.integers(0, 40, size=sz // 2 + 1)] + shared
+        keys += [pool[int(j)] for j in rng.integers(0, len(pool), size=sz)]
+        segs.append(len(keys))
+    segs = np.array(segs, np.uint64)
+    assert L.lib().rbx_tune(b"add_multi_table8", table8) == 0
+    assert L.lib().rbx_tune(b"stream_chunk", chunk) == 0
+    try:
+        counts, flags = bloom_add_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
+    finally:
+        L.lib().rbx_tune(b"add_multi_table8", 1)
+        L.lib().rbx_tune(b"stream_chunk", 0)
+    for s, t in enumerate(order):
+        sub = keys[int(segs[s]):int(segs[s + 1])]
+        c, fl = refs[t].add(*O.arena(sub), per_key=True)
+        assert counts[s] == c, s
+        assert np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl), s
+    for n, r in zip(names, refs):
+        assert client.getBloomFilter(n).exportBitmap() == r.redis_string()
+    for h in handles:
+        h.close()
+    for n in names:
+        client.getBloomFilter(n).delete()
+
+
+@pytest.mark.parametrize("table8", [1, 0])
+def test_multi_tenant_add_filter_ids_past_2_17(client, fresh, table8):
+    """per-key add parity of a multi-tenant add batch whose filter ids reach 2^17:
+    100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10) at design fill, one add_multi batch of
+    ~24 16-byte keys per tenant (a tenant's keys repeat, so shared bits occur), every tenant once in
+    tenant order except the last 1,000 segments, which revisit earlier tenants.  Per-key flags,
+    per-segment counts and all 100,000 bitmaps vs the oracle (M/RedissonBloomFilter.java:104-137)."""
+    nt = 100_000
+    rng = np.random.default_rng(0xADD17 + table8)
+    names = [f"{fresh}:{t:06d}" for t in range(nt)]
+    refs, handles = [], []
+    try:
+        for nm in names:
+            f = client.getBloomFilter(nm)
+            assert f.tryInit(1000, 1e-3)
+            nb = (f.getSize() + 7) // 8
+            bm = rng.integers(0, 256, size=nb, dtype=np.uint8)
+            f.importBitmap(bm.tobytes())
+            r = O.OracleBloom(f.getSize(), f.getHashIterations())
+            r.bitmap[:nb] = bm
+            r.redis_len = nb
+            refs.append(r)
+            handles.append(BloomHandle(client, nm))
+        assert (refs[0].size, refs[0].k) == (14_377, 10)
+        order = list(range(nt)) + [int(x) for x in rng.integers(0, nt, size=1000)]
+        sizes = rng.integers(1, 48, size=len(order))
+        segs = np.zeros(len(order) + 1, np.uint64)
+        segs[1:] = np.cumsum(sizes)
+        n = int(segs[-1])
+        pool = rng.integers(0, 256, size=(n // 2, 16), dtype=np.uint8)
+        keys = pool[rng.integers(0, len(pool), size=n)]
+        # and a key added to one tenant twice in one segment, for a few thousand segments
+        for s in range(0, len(order), 37):
+            a, b = int(segs[s]), int(segs[s + 1])
+            if b - a >= 2:
+                keys[b - 1] = keys[a]
+        assert L.lib().rbx_tune(b"add_multi_table8", table8) == 0
+        try:
+            counts, flags = bloom_add_multi(client, [handles[t] for t in order], segs, Arena.fixed(keys),
+                                            per_key=True)
+        finally:
+            L.lib().rbx_tune(b"add_multi_table8", 1)
+        for s, t in enumerate(order):
+            a, b = int(segs[s]), int(segs[s + 1])
+            c, fl = refs[t].add(*O.fixed_arena(keys[a:b]), per_key=True)
+            assert counts[s] == c and np.array_equal(flags[a:b], fl), (s, t)
+        assert int(counts.sum()) > n // 2
+        for nm, r in zip(names, refs):
+            assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
+    finally:
+        for h in handles:
+            h.close()
+        for nm in names:
+            client.getBloomFilter(nm).delete()
 
 
 def test_device_path_matches_host_path(client, fresh):

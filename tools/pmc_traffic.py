@@ -136,8 +136,9 @@ def main():
     for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_misses", "k_bk_final")),
                         ("add_pipeline", ("k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys", "k_ba_final")),
                         ("stream_pipeline", ("k_stream_compact", "k_stream_probe", "k_stream_probe8", "k_stream_contains",
-                                             "k_stream_contains_q", "k_stream_commit", "k_stream_walk",
-                                             "k_stream_final"))):
+                                             "k_stream_contains_q", "k_stream_commit", "k_stream_final8",
+                                             "k_stream_walk", "k_stream_final")),
+                        ("madd_pipeline", ("k_madd_probe8", "k_madd_final8", "k_stream_walk"))):
         # the stream pipeline runs one of its two contains kernels (staged or slot)
         parts = tuple(k for k in parts if k in out)
         if len(parts) < 3 or name not in calls:
