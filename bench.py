@@ -751,8 +751,10 @@ def run_c3(args, world, rank, local, steps, warmup):
 def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, world):
     """C3's add half: one multi-tenant add(Collection) per step -- `per` fresh random
     16-byte keys into each of the rank's tenants (rbx_bloom_add_multi_dev: the 8-byte first-setter
-    table by default).  The key window slides one key per step, so every step's (tenant, key) pairs
-    are new and the adds meet zero bits (~k/2 each at the design fill 0.5)."""
+    table by default).  The key window slides by one tenant's worth of keys per step (tenant t of step
+    s takes the keys tenant t + s took in step 0), so every step's (tenant, key) pairs are new and the
+    adds meet zero bits (~k/2 each at the design fill 0.5).  (A one-key slide keeps 999 of a tenant's
+    1,000 keys in the same tenant: after the first step almost nothing is new.)"""
     import ctypes as C
 
     import torch
@@ -762,10 +764,10 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
 
     n = per * nt
     extra = warmup + steps + 1
-    keys = torch.randint(0, 256, (n + extra, 16), dtype=torch.uint8, device="cuda", generator=g)
+    keys = torch.randint(0, 256, (n + extra * per, 16), dtype=torch.uint8, device="cuda", generator=g)
     counts = torch.zeros(nt, dtype=torch.int64, device="cuda")
     sptr = stream.cuda_stream
-    windows = [device_keys(keys.data_ptr() + 16 * j, n, 16) for j in range(extra)]
+    windows = [device_keys(keys.data_ptr() + 16 * per * j, n, 16) for j in range(extra)]
     it = [0]
 
     def step():

@@ -74,6 +74,8 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *   "add_multi_table8"      multi-tenant add: 1 (default) the 8-byte first-setter table (claims by one
  *                           CAS, replies from the first claim's slot, walk commit; when (filter id,
  *                           bit) fits 41 bits and k <= 32), 0 the 16-byte epoch-tagged table path
+ *   "walk_reset_all"        the 8-byte table's walk: bit 0 (ordered stream) / bit 1 (multi-tenant add)
+ *                           rewrites every pair EMPTY with whole-line stores; clear: only occupied pairs
  *   "stream_chunk"          ordered stream and 8-byte multi-tenant add: commands per chunk cap (0 = default: with the 8-byte
  *                           table min(2^pb - 1, 2^27 / k) rounded down to 128, else 2^26 / k)
  *   "wide_subchunk"         add / contains on a filter past 2^32 bits: keys per sub-chunk cap (0 =

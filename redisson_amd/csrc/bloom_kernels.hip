@@ -1117,7 +1117,10 @@ __global__ __launch_bounds__(256) void k_stream_occ(const unsigned long long *__
 __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restrict__ T, const uint32_t *__restrict__ nadds,
                                                      uint32_t kmax, uint32_t bb, uint32_t pb,
                                                      uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag,
-                                                     uint32_t diag = 0) {
+                                                     uint32_t diag = 0, uint32_t reset_all = 0) {
+    // reset_all: every pair is rewritten EMPTY with whole-line streaming stores (at the ~30% loads
+    // the tables run at almost every line holds an entry, and one scattered 16-byte store per
+    // occupied pair cost a partial-line write request each); 0: only occupied pairs are rewritten
     const uint32_t lg = nadds ? t8_log2(*nadds, kmax) : kmax;  // no count: kmax carries lg itself
     const uint64_t n2 = (1ULL << lg) / 2;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1125,7 +1128,10 @@ __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restr
     using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n2; q += stride) {
         u64x2 e = ((const u64x2 *)T)[q];
-        if ((e.x & e.y) == ~0ULL) continue;  // both empty
+        if ((e.x & e.y) == ~0ULL) {  // both empty
+            if (reset_all) __builtin_nontemporal_store(u64x2{~0ULL, ~0ULL}, (u64x2 *)T + q);
+            continue;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const unsigned long long v = h ? e.y : e.x;
@@ -1136,7 +1142,8 @@ __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restr
             else atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
             if (flag && !(diag & 4)) flag[v & pmask] = 1;
         }
-        ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
+        if (reset_all) __builtin_nontemporal_store(u64x2{~0ULL, ~0ULL}, (u64x2 *)T + q);
+        else ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
     }
 }
 
@@ -1714,6 +1721,10 @@ void set_stream_owner(int v) { g_stream_owner = v; }
 // lookup as one more round of its slot (in flight with the other slots' gathers), 0 inline
 static uint32_t g_stream_lookup_rounds = 1;
 void set_stream_lookup_rounds(int v) { g_stream_lookup_rounds = (uint32_t)v; }
+// rbx_tune "walk_reset_all": bit 0 = the stream's walk rewrites every pair (whole lines), bit 1 =
+// the multi-tenant add's walk does
+static uint32_t g_walk_reset_all = 0;
+void set_walk_reset_all(int v) { g_walk_reset_all = (uint32_t)v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1745,10 +1756,10 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
         hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.zmask, a.fslot, a.out, a.counts);
         hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
-                           (uint8_t *)nullptr, g_stream_diag);
+                           (uint8_t *)nullptr, g_stream_diag, g_walk_reset_all & 1u);
     } else if (a.t8) {
         hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
-                           a.flag, g_stream_diag);
+                           a.flag, g_stream_diag, g_walk_reset_all & 1u);
         hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);
     } else {
         hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
@@ -1772,7 +1783,7 @@ static void launch_madd8_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
                        a.seg_off, a.nseg, a.tile_seg0, a.t8, a.lg, a.bb, a.pb, a.zmask, a.fslot, a.out_new,
                        a.seg_counts);
     hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, (const uint32_t *)nullptr, a.lg, a.bb,
-                       a.pb, a.fid_bm, (uint8_t *)nullptr, 0u);
+                       a.pb, a.fid_bm, (uint8_t *)nullptr, 0u, (g_walk_reset_all >> 1) & 1u);
 }
 
 template <int KLEN>

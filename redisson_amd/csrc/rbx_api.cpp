@@ -3329,6 +3329,11 @@ int rbx_tune(const char *key, int value) {
         set_stream_diag(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "walk_reset_all")) {
+        if (value < 0 || value > 3) return fail(RBX_E_ILLEGAL_ARGUMENT, "walk_reset_all: bits of 1|2");
+        set_walk_reset_all(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "add_multi_table8")) {
         if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0 or 1");
         g_add_multi_t8 = value;

@@ -246,7 +246,8 @@ void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains b
 void set_stream_probe_batch(int v);
 void set_stream_diag(int v);
 void set_stream_owner(int v);          // 1 (default) replies from first-claim slots, 0 r04 owner flags
-void set_stream_lookup_rounds(int v);  // 1 (default) slot-kernel lookups as slot rounds, 0 inline  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
+void set_stream_lookup_rounds(int v);
+void set_walk_reset_all(int v);        // bit 0: stream walk, bit 1: multi-tenant add walk (whole-line resets)  // 1 (default) slot-kernel lookups as slot rounds, 0 inline  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
 void set_stream_qgrid(int v);  // slot stream-contains kernel grid (blocks)
 int get_contains_stage1();
 

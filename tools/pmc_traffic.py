@@ -32,7 +32,9 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
          ("k_ba_stage1", r"k_ba_stage1<"), ("k_ba_rebucket", r"k_ba_rebucket"), ("k_ba_region", r"k_ba_region"),
          ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
          ("k_stream_probe", r"k_stream_probe<"), ("k_stream_probe8", r"k_stream_probe8<"),
-         ("k_stream_walk", r"k_stream_walk"), ("k_stream_final", r"k_stream_final"),
+         ("k_stream_walk", r"k_stream_walk"), ("k_stream_final8", r"k_stream_final8<"),
+         ("k_stream_final", r"k_stream_final\("), ("k_madd_probe8", r"k_madd_probe8<"),
+         ("k_madd_final8", r"k_madd_final8<"),
          ("k_stream_contains_q", r"k_stream_contains_q<"),
          ("k_stream_contains", r"k_stream_contains<"),
          ("k_stream_commit", r"k_stream_commit<"),
@@ -46,7 +48,8 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
 CLASS = {"k_bk_stage1": "mixed", "k_bloom_contains": "mixed", "k_bloom_contains_multi": "mixed",
          "k_bloom_contains_q": "mixed", "k_stream_probe": "mixed", "k_stream_contains": "mixed",
          "k_stream_contains_q": "mixed",
-         "k_stream_commit": "mixed", "k_stream_probe8": "mixed", "k_gather_probe": "gather", "k_bloom_add_probe": "gather",
+         "k_stream_commit": "mixed", "k_stream_probe8": "mixed", "k_madd_probe8": "mixed", "k_gather_probe": "gather",
+         "k_bloom_add_probe": "gather",
          "k_bloom_add_commit": "gather"}  # every other kernel: stream
 
 
@@ -59,7 +62,9 @@ def short(name: str) -> str | None:
 
 def load(d: str):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    # a pass directory, or the per-pass rows kept by tools/profile_round.sh (pmc_*_rbx_rows.csv)
+    paths = [d] if os.path.isfile(d) else glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    for p in paths:
         for r in csv.DictReader(open(p)):
             s = short(r["Kernel_Name"])
             if s:
