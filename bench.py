@@ -793,8 +793,10 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
     return {"metric": "Bloom add keys/sec (whole node), C3 tenants: one add(Collection) per tenant",
             "value": sum_over_ranks(world, n) / step_s, "unit": "keys/s", "ms_per_step": step_s * 1e3,
             "keys_per_gpu": n, "new_keys_per_step": new, "steps": steps, "warmup": warmup,
-            "path": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"
-            if args.tune.find("add_multi_table8=0") < 0 else "16-byte epoch table (k_bloom_add_probe + commit)",
+            "path": {"0": "16-byte epoch table (k_bloom_add_probe + commit)",
+                     "1": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"}.get(
+                         dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv).get("add_multi_table8", "2"),
+                         "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)"),
             "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
                          "traffic": load_traffic(tj, "madd_pipeline", "hbm_bytes_by_class"),

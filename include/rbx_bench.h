@@ -71,9 +71,12 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           bits gates the lookups (one atomicOr per zero bit)
  *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
  *                           the occupancy bitmap of the table's slots, 0 (default) = none
- *   "add_multi_table8"      multi-tenant add: 1 (default) the 8-byte first-setter table (claims by one
- *                           CAS, replies from the first claim's slot, walk commit; when (filter id,
- *                           bit) fits 41 bits and k <= 32), 0 the 16-byte epoch-tagged table path
+ *   "add_multi_table8"      multi-tenant add when (filter id, bit) fits 41 bits and k <= 32: 2 (default)
+ *                           optimistic SETBITs (returning atomicOr) with a small conflict table for the
+ *                           zero bits two keys share, 1 the 8-byte first-setter table (claims by one CAS,
+ *                           replies from the first claim's slot, walk commit), 0 the 16-byte epoch table
+ *   "add_multi_conflict_log2"  entries (log2, 6..24, default 17) of the conflict table of mode 2; past
+ *                           half full the chunk's replies come from the full first-setter table
  *   "walk_reset_all"        the 8-byte table's walk: bit 0 (ordered stream) / bit 1 (multi-tenant add)
  *                           rewrites every pair EMPTY with whole-line stores; clear: only occupied pairs
  *   "stream_chunk"          ordered stream and 8-byte multi-tenant add: commands per chunk cap (0 = default: with the 8-byte

@@ -1305,6 +1305,232 @@ __global__ __launch_bounds__(256) void k_madd_final8(KeysDev keys, uint64_t base
     }
 }
 
+// ---- multi-tenant add, r05 default: optimistic SETBITs with conflict repair ---------------------
+// The first-setter table costs a CAS per zero bit and the walk an atomicOr per owned bit: 11 memory-side
+// atomics per C3 key, which bound the call (profiles/r05: 1.1G atomics per 100M-key add_multi).  But a
+// zero bit matters for the in-order replies only when two keys of the chunk share it.  So:
+//   K1 k_maddx_gather: the k bits of every key are read BEFORE any is set (zmask = zero bits);
+//   K2 k_maddx_set:    every zero bit is set with a returning atomicOr; a key that finds its zero bit
+//                      already set (another key of the chunk set it first, in execution order) records
+//                      the bit in a small conflict table C (entry (fid << bb | bit) << pb | position,
+//                      atomicMin: the smallest position among the losers);
+//   K3 k_maddx_claim:  only when C is not empty: every key registers its zero bits that are in C
+//                      (atomicMin), so C holds each shared bit's first setter in key order;
+//   K4 k_maddx_reply:  key t is new iff one of its zero bits is not in C (t is its only setter) or is
+//                      in C with first setter t.
+// Bits: the same SETBITs land (every zero bit of every key), so bitmap bytes are identical.  Replies:
+// exact (M/RedissonBloomFilter.java:104-137 with M/command/CommandBatchService.java:115-134's order).
+// C overflows (more than half full, or a probe run past 64 slots: adversarial batches of repeated keys)
+// -> K3 registers every zero bit of every key in the full 8-byte first-setter table T instead, K4
+// answers from T, and K5 empties T again.  Atomics per C3 key: ~5 (the SETBITs) instead of ~11.
+template <int KMAX>
+__device__ __forceinline__ void madd_indexes(uint64_t h1, uint64_t h2, const ModParams &mp, uint32_t zm,
+                                             uint32_t (&idxs)[KMAX]) {
+    uint64_t h = h1;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if ((zm >> j) & 1u) idxs[j] = mod63(h & 0x7fffffffffffffffULL, mp);
+        h += (j & 1) ? h1 : h2;
+    }
+}
+
+// slot of key8 in C, or -1 (linear probing; C is never more than half full when consulted)
+__device__ __forceinline__ int64_t c_find(const unsigned long long *__restrict__ C, uint32_t lgC, uint32_t pb,
+                                          uint64_t key8, unsigned long long *e_out) {
+    const uint64_t mask = (1ULL << lgC) - 1;
+    uint64_t slot = t8_slot(key8, lgC);
+    for (uint32_t probes = 0; probes < 64; ++probes) {
+        const unsigned long long e = C[slot];
+        if (e == ~0ULL) return -1;
+        if ((e >> pb) == key8) {
+            *e_out = e;
+            return (int64_t)slot;
+        }
+        slot = (slot + 1) & mask;
+    }
+    return -1;  // unreachable while the overflow rule holds (an insert past 64 probes overflows)
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_maddx_gather(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                      const FilterDesc *__restrict__ filt,
+                                                      const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                      const uint32_t *__restrict__ tile_seg0,
+                                                      uint32_t *__restrict__ zmask, unsigned long long *__restrict__ C,
+                                                      uint32_t lgC, MaddxState *__restrict__ cst) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t s = tid; s < (1ULL << lgC); s += stride) C[s] = ~0ULL;  // the previous chunk's C
+    if (tid == 0) *cst = MaddxState{0, 0};
+    for (uint64_t t = tid; t < nchunk; t += stride) {
+        const uint64_t i = base + t;
+        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t word[KMAX], idxs[KMAX];
+        uint32_t maxidx = 0;
+        uint64_t h = h1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if ((uint32_t)j < f.k) {
+                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                idxs[j] = idx;
+                word[j] = f.bm[idx >> 5];
+                maxidx = idx > maxidx ? idx : maxidx;
+            }
+            h += (j & 1) ? h1 : h2;
+        }
+        uint32_t zm = 0;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
+        zmask[t] = zm;
+        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_maddx_set(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                   const FilterDesc *__restrict__ filt,
+                                                   const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                   const uint32_t *__restrict__ tile_seg0,
+                                                   const uint32_t *__restrict__ zmask,
+                                                   unsigned long long *__restrict__ C, uint32_t lgC, uint32_t bb,
+                                                   uint32_t pb, MaddxState *__restrict__ cst) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t cmask = (1ULL << lgC) - 1;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint32_t zm = zmask[t];
+        if (!zm) continue;
+        const uint64_t i = base + t;
+        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t idxs[KMAX], old[KMAX];
+        madd_indexes<KMAX>(h1, h2, f.mp, zm, idxs);
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)  // every SETBIT in flight at once
+            if ((zm >> j) & 1u) old[j] = atomicOr(&f.bm[idxs[j] >> 5], bit_in_word(idxs[j]));
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (!((zm >> j) & 1u) || !(old[j] & bit_in_word(idxs[j]))) continue;
+            // lost the race for a zero bit: another key of the chunk shares it
+            const uint64_t key8 = ((uint64_t)f.fid << bb) | idxs[j];
+            const unsigned long long mine = ((unsigned long long)key8 << pb) | t;
+            uint64_t slot = t8_slot(key8, lgC);
+            bool done = false;
+            for (uint32_t probes = 0; probes < 64 && !done; ++probes) {
+                const unsigned long long o = atomicCAS(&C[slot], ~0ULL, mine);
+                if (o == ~0ULL) {
+                    if (atomicAdd(&cst->count, 1u) + 1 > (uint32_t)(cmask >> 1)) atomicOr(&cst->overflow, 1u);
+                    done = true;
+                } else if ((o >> pb) == key8) {
+                    if (o > mine) atomicMin(&C[slot], mine);
+                    done = true;
+                } else {
+                    slot = (slot + 1) & cmask;
+                }
+            }
+            if (!done) atomicOr(&cst->overflow, 1u);
+        }
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_maddx_claim(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                     const FilterDesc *__restrict__ filt,
+                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                     const uint32_t *__restrict__ tile_seg0,
+                                                     const uint32_t *__restrict__ zmask,
+                                                     unsigned long long *__restrict__ C, uint32_t lgC,
+                                                     unsigned long long *__restrict__ T, uint32_t lgT, uint32_t bb,
+                                                     uint32_t pb, const MaddxState *__restrict__ cst, uint32_t batch) {
+    const MaddxState cs = *cst;
+    if (cs.count == 0 && !cs.overflow) return;  // no shared zero bit: every key with one is new
+    const uint64_t pmask = (1ULL << pb) - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
+        const uint32_t zm = zmask[t];
+        if (!zm) continue;
+        const uint64_t i = base + t;
+        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
+        uint64_t h1, h2;
+        hash_key<KLEN>(keys, i, h1, h2);
+        uint32_t idxs[KMAX];
+        madd_indexes<KMAX>(h1, h2, f.mp, zm, idxs);
+        if (cs.overflow) {  // every zero bit into the full first-setter table
+            (void)t8_claim<KMAX>(T, lgT, bb, pb, f.fid, idxs, zm, (uint32_t)t, batch);
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (!((zm >> j) & 1u)) continue;
+            const uint64_t key8 = ((uint64_t)f.fid << bb) | idxs[j];
+            unsigned long long e;
+            const int64_t slot = c_find(C, lgC, pb, key8, &e);
+            if (slot >= 0 && (e & pmask) > t) atomicMin(&C[slot], ((unsigned long long)key8 << pb) | t);
+        }
+    }
+}
+
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_maddx_reply(KeysDev keys, uint64_t base, uint64_t nchunk,
+                                                     const FilterDesc *__restrict__ filt,
+                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
+                                                     const uint32_t *__restrict__ tile_seg0,
+                                                     const uint32_t *__restrict__ zmask,
+                                                     const unsigned long long *__restrict__ C, uint32_t lgC,
+                                                     const unsigned long long *__restrict__ T, uint32_t lgT,
+                                                     uint32_t bb, uint32_t pb, const MaddxState *__restrict__ cst,
+                                                     uint8_t *__restrict__ out_new,
+                                                     unsigned long long *__restrict__ seg_counts) {
+    const MaddxState cs = *cst;
+    const uint64_t pmask = (1ULL << pb) - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n_up = (nchunk + 63) & ~63ULL;  // whole waves (wave_seg_add)
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_up; t += stride) {
+        const bool in = t < nchunk;
+        const uint64_t i = base + t;
+        uint32_t seg = 0;
+        bool isnew = false;
+        if (in) {
+            seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
+            const uint32_t zm = zmask[t];
+            if (zm && cs.count == 0 && !cs.overflow) {
+                isnew = true;
+            } else if (zm) {
+                const FilterDesc f = filt[seg];
+                uint64_t h1, h2;
+                hash_key<KLEN>(keys, i, h1, h2);
+                uint32_t idxs[KMAX];
+                madd_indexes<KMAX>(h1, h2, f.mp, zm, idxs);
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (!((zm >> j) & 1u) || isnew) continue;
+                    const uint64_t key8 = ((uint64_t)f.fid << bb) | idxs[j];
+                    if (cs.overflow) {
+                        isnew = t8_find(T, lgT, pb, key8) == (uint32_t)t;
+                    } else {
+                        unsigned long long e;
+                        isnew = c_find(C, lgC, pb, key8, &e) < 0 || (e & pmask) == t;
+                    }
+                }
+            }
+            if (out_new) out_new[i] = isnew;
+        }
+        if (seg_counts) wave_seg_add(in, seg, isnew ? 1u : 0u, seg_counts);
+    }
+}
+
+// after an overflowed chunk: T back to EMPTY (its bits were set by k_maddx_set already)
+__global__ __launch_bounds__(256) void k_maddx_reset(unsigned long long *__restrict__ T, uint32_t lgT,
+                                                     const MaddxState *__restrict__ cst) {
+    if (!cst->overflow) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < (1ULL << lgT); s += stride)
+        if (T[s] != ~0ULL) T[s] = ~0ULL;
+}
+
 // ---- single-filter fast path: 8-byte entries (bit << 32 | key id), empty = ~0 ------------
 // The table is cleared (memset 0xff) before every chunk, so a claim is one CAS on an empty
 // slot; a slot already holding the same bit takes the 64-bit atomicMin (same high word, so
@@ -1786,8 +2012,30 @@ static void launch_madd8_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
                        a.pb, a.fid_bm, (uint8_t *)nullptr, 0u, (g_walk_reset_all >> 1) & 1u);
 }
 
+template <int KLEN, int KMAX>
+static void launch_maddx_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
+    const unsigned grid = grid_for(std::max<uint64_t>(a.nchunk, 1ULL << a.lgC), kMaxGrid);
+    hipLaunchKernelGGL((k_maddx_gather<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.cst);
+    hipLaunchKernelGGL((k_maddx_set<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.bb, a.pb, a.cst);
+    hipLaunchKernelGGL((k_maddx_claim<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst,
+                       g_probe8_batch);
+    hipLaunchKernelGGL((k_maddx_reply<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst, a.out_new,
+                       a.seg_counts);
+    hipLaunchKernelGGL(k_maddx_reset, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.lg, a.cst);
+}
+
 template <int KLEN>
 static void launch_madd8_chunk_len(const MaddChunkArgs &a, hipStream_t st) {
+    if (a.c8) {
+        if (a.kmax <= 8) launch_maddx_chunk_k<KLEN, 8>(a, st);
+        else if (a.kmax <= 16) launch_maddx_chunk_k<KLEN, 16>(a, st);
+        else launch_maddx_chunk_k<KLEN, 32>(a, st);
+        return;
+    }
     if (a.kmax <= 8) launch_madd8_chunk_k<KLEN, 8>(a, st);
     else if (a.kmax <= 16) launch_madd8_chunk_k<KLEN, 16>(a, st);
     else launch_madd8_chunk_k<KLEN, 32>(a, st);

@@ -190,6 +190,7 @@ struct rbx_ctx {
     DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
     DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
     DevBuf st_fslot;             // ordered stream (r05): per add, the slot of its first zero bit's claim
+    DevBuf madd_c;               // multi-tenant add (r05): conflict table C + its MaddxState
     uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
     uint64_t st_geom[4] = {0, 0, 0, 0};             // last stream call: bb, fbits, pb, chunk
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
@@ -890,7 +891,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot}) {
+                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot, &c->madd_c}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -1594,9 +1595,13 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
 // rbx_tune("stream_chunk", n) caps a chunk of the ordered stream and of the 8-byte multi-tenant add at
 // n commands (tests: many chunks on small batches).
 static uint64_t g_stream_chunk = 0;
-// rbx_tune("add_multi_table8"): 1 (default) multi-tenant adds on the 8-byte first-setter table
-// (k_madd_*, r05) whenever (filter id, bit) fits 41 bits and k <= 32; 0 the r03 16-byte table path
-static int g_add_multi_t8 = 1;
+// rbx_tune("add_multi_table8"): multi-tenant adds whenever (filter id, bit) fits 41 bits and k <= 32:
+// 2 (default) optimistic SETBITs with conflict repair (k_maddx_*, r05), 1 the 8-byte first-setter table
+// with the walk commit (k_madd_*, r05), 0 the r03 16-byte table path
+static int g_add_multi_t8 = 2;
+// rbx_tune("add_multi_conflict_log2"): entries of the conflict table C, log2 (default 17: 1 MiB, L2-
+// resident; tests use small ones to run the overflow path)
+static uint32_t g_maddx_lgc = 17;
 
 // Multi-tenant add on the 8-byte table: chunks of <= min(2^pb - 1, 2^27 / k) keys, each probe ->
 // final -> walk, in key order (a chunk's bits are set before the next probes).  The table and its
@@ -1618,6 +1623,8 @@ static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg
     }
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_fslot.reserve(chunk * 4));
+    const bool optimistic = g_add_multi_t8 == 2;
+    if (optimistic) RBX_TRY(c->madd_c.reserve((8ULL << g_maddx_lgc) + 64));
     struct ResetOnError {  // see rbx_bloom_stream_dev
         rbx_ctx *c;
         bool ok = false;
@@ -1645,6 +1652,11 @@ static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg
         a.fslot = c->st_fslot.as<uint32_t>();
         a.out_new = d_out_new;
         a.seg_counts = d_seg_counts;
+        if (optimistic) {
+            a.c8 = c->madd_c.as<unsigned long long>();
+            a.lgC = g_maddx_lgc;
+            a.cst = (MaddxState *)(a.c8 + (1ULL << g_maddx_lgc));
+        }
         launch_madd8_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
     }
@@ -3335,8 +3347,13 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     if (!strcmp(key, "add_multi_table8")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0 or 1");
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0, 1 or 2");
         g_add_multi_t8 = value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_multi_conflict_log2")) {
+        if (value < 6 || value > 24) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_conflict_log2 in [6, 24]");
+        g_maddx_lgc = (uint32_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_owner")) {

@@ -175,6 +175,11 @@ struct StreamChunkArgs {
     uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks; stream_owner 0)
     uint32_t *fslot;              // per add-list entry: the table slot of its first zero bit's claim (r05)
 };
+// state of the optimistic multi-tenant add's conflict table (k_maddx_*), reset per chunk
+struct MaddxState {
+    uint32_t count;     // entries inserted into C
+    uint32_t overflow;  // C too full (or a probe run too long): the full table T decides the chunk
+};
 // One chunk of a multi-tenant add on the 8-byte first-setter table (r05, bloom_kernels.hip k_madd_*):
 // probe (claims) -> final (replies, per-segment counts) -> walk (OR owned bits, empty the table).
 struct MaddChunkArgs {
@@ -191,6 +196,11 @@ struct MaddChunkArgs {
     uint32_t *zmask, *fslot;  // per key of the chunk
     uint8_t *out_new;
     unsigned long long *seg_counts;
+    // r05 optimistic SETBITs with conflict repair (k_maddx_*): non-null = that path, with the small
+    // conflict table C of 2^lgC entries and its state word; t8 / lg then serve only an overflowed chunk
+    unsigned long long *c8;
+    uint32_t lgC;
+    MaddxState *cst;
 };
 void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st);
 // entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)

@@ -332,15 +332,17 @@ def test_multi_tenant_parity(client, fresh):
         client.getBloomFilter(n).delete()
 
 
-@pytest.mark.parametrize("table8", [1, 0])
+@pytest.mark.parametrize("table8,clog2", [(2, 17), (2, 6), (1, 17), (0, 17)])
 @pytest.mark.parametrize("chunk", [0, 700])
-def test_multi_tenant_add_first_setter_tables(client, fresh, table8, chunk):
-    """r05: multi-tenant add(Collection) on the 8-byte first-setter table (add_multi_table8 1, default:
-    one CAS per zero bit, replies from the first claim's slot, walk commit) and on the r03 16-byte
-    table (0).  Shapes with k up to 17 (KMAX 32), variable-length keys (KLEN 0), repeated tenants
-    and keys repeated inside and across segments (shared bits: the final pass's slow path); chunk
-    700 runs the 8-byte path in many chunks (the in-order fold across chunk boundaries)."""
-    rng = np.random.default_rng(1200 + table8 + chunk)
+def test_multi_tenant_add_first_setter_tables(client, fresh, table8, clog2, chunk):
+    """r05: multi-tenant add(Collection) by optimistic SETBITs with conflict repair (add_multi_table8 2,
+    default; a 64-entry conflict table (clog2 6) overflows and the chunk falls back to the full
+    first-setter table), on the 8-byte first-setter table (1: one CAS per zero bit, replies from the
+    first claim's slot, walk commit) and on the r03 16-byte table (0).  Shapes with k up to 17 (KMAX
+    32), variable-length keys (KLEN 0), repeated tenants and keys repeated inside and across segments
+    (shared zero bits); chunk 700 runs the chunked paths in many chunks (the in-order fold across
+    chunk boundaries)."""
+    rng = np.random.default_rng(1200 + table8 + chunk + clog2)
     names = [f"{fresh}-{t}" for t in range(6)]
     shapes = [(14377587, 10), (729, 5), (9585, 7), (64, 7), (1 << 20, 3), (100003, 17)]
     refs = []
@@ -358,11 +360,13 @@ def test_multi_tenant_add_first_setter_tables(client, fresh, table8, chunk):
         segs.append(len(keys))
     segs = np.array(segs, np.uint64)
     assert L.lib().rbx_tune(b"add_multi_table8", table8) == 0
+    assert L.lib().rbx_tune(b"add_multi_conflict_log2", clog2) == 0
     assert L.lib().rbx_tune(b"stream_chunk", chunk) == 0
     try:
         counts, flags = bloom_add_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
     finally:
-        L.lib().rbx_tune(b"add_multi_table8", 1)
+        L.lib().rbx_tune(b"add_multi_table8", ADD_MULTI_DEFAULT)
+        L.lib().rbx_tune(b"add_multi_conflict_log2", 17)
         L.lib().rbx_tune(b"stream_chunk", 0)
     for s, t in enumerate(order):
         sub = keys[int(segs[s]):int(segs[s + 1])]
@@ -377,7 +381,10 @@ def test_multi_tenant_add_first_setter_tables(client, fresh, table8, chunk):
         client.getBloomFilter(n).delete()
 
 
-@pytest.mark.parametrize("table8", [1, 0])
+ADD_MULTI_DEFAULT = 2
+
+
+@pytest.mark.parametrize("table8", [2, 1, 0])
 def test_multi_tenant_add_filter_ids_past_2_17(client, fresh, table8):
     """per-key add parity of a multi-tenant add batch whose filter ids reach 2^17:
     100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10) at design fill, one add_multi batch of
@@ -418,7 +425,7 @@ def test_multi_tenant_add_filter_ids_past_2_17(client, fresh, table8):
             counts, flags = bloom_add_multi(client, [handles[t] for t in order], segs, Arena.fixed(keys),
                                             per_key=True)
         finally:
-            L.lib().rbx_tune(b"add_multi_table8", 1)
+            L.lib().rbx_tune(b"add_multi_table8", ADD_MULTI_DEFAULT)
         for s, t in enumerate(order):
             a, b = int(segs[s]), int(segs[s + 1])
             c, fl = refs[t].add(*O.fixed_arena(keys[a:b]), per_key=True)

@@ -24,7 +24,7 @@ timeout -s KILL 240 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum --kernel-t
 # API calls per bench run: warmup 2 + steps 5 of the measured op; C2 also adds twice (scratch warm-up + setup),
 # and its tryInit(448_089_842, 0.01) filter adds once and contains 4 times (extra.c2_tryinit_nonpow2)
 python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_tcc" "$OUT/pmc_req" "$OUT/pmc_atomic" -o "$OUT/traffic.json" \
-  --calls contains_pipeline=11 add_pipeline=3 stream_pipeline=7 madd_pipeline=7 --stream-bytes $SB > /dev/null || exit 1
+  --calls contains_pipeline=11 add_pipeline=3 stream_pipeline=7 madd_pipeline=7 maddx_pipeline=7 --stream-bytes $SB > /dev/null || exit 1
 # keep summaries only (gpurun copies back <= 64 MiB): stats CSVs, our kernels' counter rows
 for d in pmc_fetch pmc_write pmc_tcc pmc_req pmc_atomic; do
   f=$(find "$OUT/$d" -name "*counter_collection.csv" | head -1)
