@@ -789,6 +789,8 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
     # a key + k x 8 B gathered + k x 8 B RMW
     algo = n * (16 + 2 * k * 8)
     tj = args.traffic_json if (args.keys, args.tenants, world) == (100_000_000, 100_000, 1) else None
+    mode = dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv).get("add_multi_table8", "2")
+    pipe = {"1": "madd_pipeline", "0": None}.get(mode, "maddx_pipeline")
     del keys
     return {"metric": "Bloom add keys/sec (whole node), C3 tenants: one add(Collection) per tenant",
             "value": sum_over_ranks(world, n) / step_s, "unit": "keys/s", "ms_per_step": step_s * 1e3,
@@ -799,9 +801,10 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
                          "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)"),
             "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
-                         "traffic": load_traffic(tj, "madd_pipeline", "hbm_bytes_by_class"),
-                         "requests_per_launch": load_traffic(tj, "madd_pipeline", "requests_per_launch"),
-                         "atomic_requests_per_launch": load_traffic(tj, "madd_pipeline", "atomic_requests_per_launch")}}
+                         "traffic": load_traffic(tj, pipe, "hbm_bytes_by_class") if pipe else None,
+                         "requests_per_launch": load_traffic(tj, pipe, "requests_per_launch") if pipe else None,
+                         "atomic_requests_per_launch": load_traffic(tj, pipe, "atomic_requests_per_launch")
+                         if pipe else None}}
 
 
 # ------------------------------------------------------------------------------------------
