@@ -34,6 +34,43 @@ def timed(stream, fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
+def murmur64a_16(mat):
+    """MurmurHash64A (seed 0xadc83b19, redis hyperloglog.c) of 16-byte rows, vectorized (numpy u64)."""
+    import numpy as np
+
+    m, r = np.uint64(0xC6A4A7935BD1E995), np.uint64(47)
+    with np.errstate(over="ignore"):
+        h = np.uint64(0xADC83B19) ^ (np.uint64(16) * m)
+        h = np.full(mat.shape[0], h, dtype=np.uint64)
+        for b in range(2):
+            k = mat[:, 8 * b:8 * b + 8].copy().view(np.uint64).reshape(-1)
+            k = k * m
+            k ^= k >> r
+            k = k * m
+            h ^= k
+            h = h * m
+        h ^= h >> r
+        h = h * m
+        h ^= h >> r
+    return h
+
+
+def murmur_count1_elements(indexes, rng):
+    """One 16-byte element per register index with hllPatLen count 1 (bit 14 of the hash set)."""
+    import numpy as np
+
+    want, found = set(int(i) for i in indexes), {}
+    while len(found) < len(want):
+        cand = rng.integers(0, 256, size=(1 << 20, 16), dtype=np.uint8)
+        h = murmur64a_16(cand)
+        ok = ((h >> np.uint64(14)) & np.uint64(1)) == np.uint64(1)
+        for j in np.nonzero(ok)[0]:
+            i = int(h[j] & np.uint64(16383))
+            if i in want and i not in found:
+                found[i] = cand[j]
+    return np.stack([found[i] for i in sorted(want)])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="*", default=["gather", "stage1", "sizes", "add"])
@@ -347,6 +384,49 @@ def main():
             for hp in hs:
                 L.lib().rbx_hll_close(C.c_void_p(hp))
             del el
+
+    if "hllruns" in a.what:
+        # the sparse replay's residual case.  10k fresh HLLs, three multi-key PFADD
+        # batches (tests/test_hll_gpu.py::test_sparse_first_batches_many_keys at 10k keys): 1,000 and
+        # 150 random 16-byte elements per key (the normalized-string shortcut), then 20 per key plus,
+        # on every third key, five elements raising registers 5000..5004 to 1 in descending order
+        # (a run of five equal registers: element-by-element replay).  Time of each batch.
+        import ctypes as C
+
+        import numpy as np
+
+        NH = 10_000
+        rng = np.random.default_rng(67)
+        run5 = murmur_count1_elements(range(5000, 5005), rng)[::-1]
+        hs = []
+        for i in range(NH):
+            hp = C.c_void_p()
+            assert L.lib().rbx_hll_open(client.ctx, f"hr-{i}".encode(), 1, C.byref(hp)) == 0
+            hs.append(hp.value)
+        arr = (C.c_void_p * NH)(*hs)
+        out = {"bench": "hllruns", "hlls": NH}
+        for tag, per, extra in (("first", 1000, False), ("second", 150, False), ("third", 20, True)):
+            els = [rng.integers(0, 256, size=(per, 16), dtype=np.uint8) for _ in range(NH)]
+            if extra:
+                for i in range(0, NH, 3):
+                    els[i] = np.concatenate([els[i], run5])
+            seg = np.zeros(NH + 1, np.uint64)
+            seg[1:] = np.cumsum([len(e) for e in els])
+            el = torch.from_numpy(np.concatenate(els)).cuda()
+            changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
+            dk = device_keys(el.data_ptr(), int(seg[-1]), 16)
+            torch.cuda.synchronize()
+            out[tag + "_ms"] = timed(stream, lambda: L.lib().rbx_hll_add_multi_dev(
+                client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk), changed.data_ptr(), sp), 1)
+            buf = np.zeros(16 + 12288, np.uint8)
+            ln = C.c_uint64()
+            assert L.lib().rbx_hll_export_enc(client.ctx, b"hr-0", 2, buf.ctypes.data_as(L.u8p), buf.size,
+                                              C.byref(ln)) == 0
+            out[tag + "_hll0"] = ("sparse" if buf[4] else "dense", int(ln.value))
+        out["third_over_first"] = out["third_ms"] / out["first_ms"]
+        print(json.dumps(out), flush=True)
+        for hp in hs:
+            L.lib().rbx_hll_close(C.c_void_p(hp))
 
     if "addab" in a.what:
         # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
