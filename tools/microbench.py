@@ -427,6 +427,40 @@ def main():
         print(json.dumps(out), flush=True)
         for hp in hs:
             L.lib().rbx_hll_close(C.c_void_p(hp))
+        # first batches that leave the shortcut: runs of five in a 1,000-element batch, and batches
+        # near the size limit (the B bound fails, the fewest-bytes encoding still fits)
+        for per, runs in ((1000, False), (1000, True), (1300, False), (1500, False), (1700, False)):
+            hs = []
+            for i in range(NH):
+                hp = C.c_void_p()
+                assert L.lib().rbx_hll_open(client.ctx, f"hq-{per}-{int(runs)}-{i}".encode(), 1, C.byref(hp)) == 0
+                hs.append(hp.value)
+            arr = (C.c_void_p * NH)(*hs)
+            els = [rng.integers(0, 256, size=(per, 16), dtype=np.uint8) for _ in range(NH)]
+            if runs:
+                for i in range(0, NH, 3):
+                    els[i] = np.concatenate([els[i], run5])
+            seg = np.zeros(NH + 1, np.uint64)
+            seg[1:] = np.cumsum([len(e) for e in els])
+            el = torch.from_numpy(np.concatenate(els)).cuda()
+            changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
+            dk = device_keys(el.data_ptr(), int(seg[-1]), 16)
+            torch.cuda.synchronize()
+            ms = timed(stream, lambda: L.lib().rbx_hll_add_multi_dev(
+                client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk), changed.data_ptr(), sp), 1)
+            enc = []
+            for i in (0, 1):
+                buf = np.zeros(16 + 12288, np.uint8)
+                ln = C.c_uint64()
+                assert L.lib().rbx_hll_export_enc(client.ctx, f"hq-{per}-{int(runs)}-{i}".encode(), 2,
+                                                  buf.ctypes.data_as(L.u8p), buf.size, C.byref(ln)) == 0
+                enc.append(("sparse" if buf[4] else "dense", int(ln.value)))
+            print(json.dumps({"bench": "hllruns_first", "hlls": NH, "per": per, "runs_of_five": runs, "ms": ms,
+                              "hll0_hll1": enc}), flush=True)
+            for hp in hs:
+                L.lib().rbx_hll_close(C.c_void_p(hp))
+            for i in range(NH):
+                client.getHyperLogLog(f"hq-{per}-{int(runs)}-{i}").delete()
 
     if "addab" in a.what:
         # C2 add (n/2 keys into an empty 2^32-bit filter), rbx_tune variants interleaved round by
