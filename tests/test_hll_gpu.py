@@ -623,3 +623,78 @@ def test_c4_10k_hlls_three_pool_chunks(client, fresh):
             L.lib().rbx_hll_close(h)
     for nm in keys:
         client.getHyperLogLog(nm).delete()
+
+
+def _shortcut_case(kind, rng):
+    """Element lists (16-byte, count-1 or count-2 elements at chosen registers) for the boundaries of
+    the normalized-string shortcut (hll_kernels.hip replay_one): the shortcut applies when
+    the final registers have no nonzero run longer than 4 and 16 + B <= 3000 (B = bytes of the maximal
+    zero runs + one byte per nonzero register)."""
+    if kind == "runs_of_exactly_4":
+        # registers 100..103 -> 1 and 300..303 -> 2: runs of exactly four equal registers
+        els = _count1_elements(range(100, 104), rng) + _count_elements(range(300, 304), 2, rng)
+        els += _count1_elements(rng.choice(np.arange(1000, 16000), size=200, replace=False), rng)
+    elif kind == "B_exactly_2984":
+        # registers 1, 3, ..., 2981 -> 1: B = 1491 VALs + 1491 ZERO(1) + a 2-byte XZERO = 2984
+        els = _count1_elements(range(1, 2982, 2), rng)
+    elif kind == "B_2985_promotes":
+        # one nonzero register more (2983): 16 + B = 3002, and no encoding of the registers is shorter
+        els = _count1_elements(range(1, 2984, 2), rng)
+    elif kind == "pairs_past_B_within_fewest":
+        # registers 3i, 3i+1 -> 1 for i < 1000: B = 3002 (shortcut off), the fewest-bytes encoding (VAL(1,2)
+        # per pair) ~2002: neither shortcut decides, the element-by-element replay does
+        idx = np.sort(np.concatenate([np.arange(0, 3000, 3), np.arange(1, 3000, 3)]))
+        els = _count1_elements(idx, rng)
+    else:
+        raise AssertionError(kind)
+    order = rng.permutation(len(els))
+    return [els[int(i)] for i in order]
+
+
+@pytest.mark.parametrize("kind", ["runs_of_exactly_4", "B_exactly_2984", "B_2985_promotes",
+                                  "pairs_past_B_within_fewest"])
+def test_sparse_shortcut_boundaries(client, fresh, kind):
+    """byte-level checks at the boundaries of the sparse-replay shortcut -- runs of exactly
+    four equal registers, B exactly at the limit (16 + B = 3000) and one register past it, and strings
+    whose B is past the limit while their fewest-bytes encoding fits (element-by-element replay).  One
+    PFADD per key, elements in random order; the GET bytes equal the hllSparseSet restatement
+    (oracle RedisHll; Redis's hyperloglog.c itself is not in the reference: parity with a live Redis
+    stays unpinned)."""
+    rng = np.random.default_rng(abs(hash(kind)) % (1 << 32))
+    els = _shortcut_case(kind, rng)
+    h = client.getHyperLogLog(fresh)
+    assert h.addAll(Arena(els)) is True
+    ref = O.RedisHll()
+    ref.pfadd(*O.arena(els))
+    s = h.exportString()
+    assert s == ref.string(s[8:16])
+    if kind == "B_exactly_2984":
+        assert s[4] == 1 and len(s) == 3000
+    if kind == "B_2985_promotes":
+        assert s[4] == 0
+    h.delete()
+
+
+@pytest.mark.parametrize("lead", [0, 1])
+def test_sparse_set_string_just_under_the_limit(client, fresh, lead):
+    """a SET (imported) sparse string of 2,999 / 3,000 bytes (normalized: 1,491 VAL(1,1) with a
+    ZERO(1) between neighbours from register `lead`, a leading ZERO(1) when lead = 1, then one XZERO),
+    then PFADDs that raise VALs in place (no growth), fill ZERO(1)s between VALs of another value (no
+    growth) and split the XZERO (growth past the limit -> dense)."""
+    rng = np.random.default_rng(400 + lead)
+    regs = O.hll_new()
+    regs[lead:lead + 2 * 1491:2] = 1
+    ops = _sparse_encode(regs)
+    s0 = _header(1, bytes(7) + b"\x80") + ops
+    assert len(s0) == 2999 + lead
+    h = client.getHyperLogLog(fresh)
+    h.importString(s0)
+    ref = O.RedisHll.from_string(s0)
+    for batch in (_count_elements([lead, lead + 2, lead + 4], 2, rng), _count1_elements([lead + 1, lead + 3], rng),
+                  _count1_elements([12000], rng)):
+        h.addAll(Arena(batch))
+        ref.pfadd(*O.arena(batch))
+        s = h.exportString()
+        assert s == ref.string(s[8:16])
+    assert s[4] == 0  # the split of the XZERO grew the string past the limit
+    h.delete()
