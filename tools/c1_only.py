@@ -1,10 +1,11 @@
 """C1 leg alone (for rocprofv3): tryInit(1e7, 0.01), add 1M 16-byte keys into a fresh filter and
 contains 2M, `reps` times -- the calls bench.py's run_c1 times."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from redisson_amd import BloomHandle, RedissonClient, device_keys  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
