@@ -12,13 +12,13 @@
 //   B  k_ba_rebucket: level 1 -> regions (idx >> 16), fan-out <= 256
 //   C  k_ba_region  : region bitmap + met-once / met-again bitsets + a collision table in LDS;
 //                     owners set their bits; the bitmap is written back
-//   D  k_ba_keys    : non-owner counters -> new_bits;  D' k_ba_keys_rec: owner records -> new_bits
-//   E  k_ba_final   : out_new bytes and the count
+//   D  k_ba_keys_rec: owner records -> new_bits
+//   E  k_ba_final   : out_new bytes and the count (non-owner counters decoded here, r05)
 // Reporting new keys: a key is new iff at least one of its k pairs owns its bit.  k_ba_mode
 // samples the bitmap's fill per chunk and picks (rbx_tune "add_records" can force one):
 //   - below a fill of 3/32 each NON-OWNER pair bumps its key's byte counter with one
 //     fire-and-forget atomic (C2 into an empty filter: only the ~4% in-batch collisions do) and
-//     D turns counters into new bits (count < k);
+//     E turns counters into replies (count < k);
 //   - otherwise the region kernel writes the OWNER pairs' key ids as runs bucketed by 2^20-key
 //     range (one reservation per range per region) and D' sets their bits in LDS images of the
 //     ranges' new_bits words -- streaming instead of one scattered atomic per report, so the
@@ -324,9 +324,21 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
 // mode -----------------------------------------------------------------------------------
 // Sampled fill of the bitmap -> how C reports new keys (see the header): 1 = non-owner counters,
 // 2 = owner records, 0 = owner bits.
+// r05: every block also zeroes the chunk's counters (zero_a: cnt1 .. overflow, not the mode word)
+// and new_bits (zero_b) -- two hipMemsetAsync fills (~5 us each on the C1 add) folded into this
+// launch.
 __global__ __launch_bounds__(1024) void k_ba_mode(const uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t policy,
-                                                  uint32_t *__restrict__ mode) {
+                                                  uint32_t *__restrict__ mode, uint32_t *__restrict__ zero_a,
+                                                  uint64_t na, uint32_t *__restrict__ zero_b, uint64_t nb) {
     __shared__ uint32_t s_sum[16];
+    {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) zero_a[i] = 0u;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb / 4; i += stride)
+            ((u32x4 *)zero_b)[i] = u32x4{0u, 0u, 0u, 0u};
+        if (blockIdx.x == 0 && threadIdx.x < (nb & 3)) zero_b[(nb & ~3ULL) + threadIdx.x] = 0u;
+    }
+    if (blockIdx.x != 0) return;  // uniform: the mode is block 0's
     uint32_t c = 0;
     if (policy == 2) {
         constexpr uint32_t kSamples = 4096;
@@ -873,28 +885,6 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
 }
 
 // D ------------------------------------------------------------------------------------
-// Non-owner counters -> new_bits (a key is new iff fewer than k of its pairs were non-owners);
-// the counters read are zeroed for the next call.  Owner bits need nothing here.
-__global__ __launch_bounds__(256) void k_ba_keys(uint32_t *__restrict__ ctr, uint64_t nchunk, uint32_t k,
-                                                 uint32_t *__restrict__ new_bits, const uint32_t *__restrict__ overflow,
-                                                 const uint32_t *__restrict__ mode) {
-    if (*overflow || *mode != 1) return;
-    const uint64_t nw = (nchunk + 31) >> 5;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x) {
-        u32x4 *src = (u32x4 *)(ctr + 8 * w);
-        const u32x4 a = src[0], b = src[1];
-        const uint32_t c8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint32_t v = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-#pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) v |= (((c8[j] >> (8 * t)) & 0xffu) < k ? 1u : 0u) << (4 * j + t);
-        new_bits[w] = v;
-        if (a.x | a.y | a.z | a.w) src[0] = u32x4{0u, 0u, 0u, 0u};
-        if (b.x | b.y | b.z | b.w) src[1] = u32x4{0u, 0u, 0u, 0u};
-    }
-}
-
 // Owner records -> new_bits: item = (key range q, slice s of 2^20 records): the slice's key ids
 // set bits of a 128 KiB LDS image of the range's new_bits words, whose nonzero words are OR-ed in.
 constexpr uint32_t kBaRangeWords = 1u << (kBaKeyRangeBits - 5);  // 32768
@@ -944,24 +934,54 @@ __global__ __launch_bounds__(1024) void k_ba_keys_rec(const uint32_t *__restrict
 }
 
 // E ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_final(const uint32_t *__restrict__ new_bits, uint64_t nchunk,
-                                                  uint64_t base, uint8_t *__restrict__ out_new,
+// Replies and the count, one thread per 32 keys.  Non-owner counters (mode 1) are read here
+// directly -- key t is new iff fewer than k of its pairs were non-owners -- and zeroed for the next
+// call (r05: the separate k_ba_keys pass and its launch are gone); owner bits / records (modes 0,
+// 2) arrive as new_bits.
+__global__ __launch_bounds__(256) void k_ba_final(const uint32_t *__restrict__ new_bits, uint32_t *__restrict__ ctr,
+                                                  uint32_t k, uint64_t nchunk, uint64_t base,
+                                                  uint8_t *__restrict__ out_new,
                                                   unsigned long long *__restrict__ count,
-                                                  const uint32_t *__restrict__ overflow) {
+                                                  const uint32_t *__restrict__ overflow,
+                                                  const uint32_t *__restrict__ mode) {
     __shared__ unsigned long long s_part[4];
     if (*overflow) return;
+    const bool counters = *mode == 1u;
     unsigned long long c = 0;
     const uint64_t nwords = (nchunk + 31) >> 5;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nwords; g += stride) {
-        uint32_t v = new_bits[g];
+        uint32_t v = 0;
+        if (counters) {
+            u32x4 *src = (u32x4 *)(ctr + 8 * g);
+            const u32x4 a = src[0], b = src[1];
+            const uint32_t c8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) v |= (((c8[j] >> (8 * t)) & 0xffu) < k ? 1u : 0u) << (4 * j + t);
+            if (a.x | a.y | a.z | a.w) src[0] = u32x4{0u, 0u, 0u, 0u};
+            if (b.x | b.y | b.z | b.w) src[1] = u32x4{0u, 0u, 0u, 0u};
+        } else {
+            v = new_bits[g];
+        }
         const uint64_t rem = nchunk - (g << 5);
         if (rem < 32) v &= (1u << rem) - 1u;
         c += __popc(v);
+        if (out_new) {
+            uint8_t *o = out_new + base + (g << 5);
+            if (rem >= 32 && ((uintptr_t)o & 3) == 0) {
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const uint32_t nib = (v >> (4 * q)) & 0xfu;
+                    ((uint32_t *)o)[q] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+                }
+            } else {
+                const uint32_t m = rem < 32 ? (uint32_t)rem : 32u;
+                for (uint32_t q = 0; q < m; ++q) o[q] = (uint8_t)((v >> q) & 1u);
+            }
+        }
     }
-    if (out_new)
-        for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride)
-            out_new[base + t] = (uint8_t)((new_bits[t >> 5] >> (t & 31)) & 1u);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
     if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = c;
@@ -997,8 +1017,11 @@ template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
     constexpr int TILE = kBaS1Threads * ba_per<KMAX>();
     const uint64_t ntiles = (a.nchunk + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_ba_mode, dim3(1), dim3(1024), 0, st, (const uint32_t *)a.f.bm, a.nwords4, a.record_policy,
-                       a.mode);
+    // (the mode word is the last counter word: zeroed by nobody, written by block 0)
+    const uint64_t na = (uint64_t)(a.mode - a.cnt1), nb = (uint64_t)a.nranges << (kBaKeyRangeBits - 5);
+    const unsigned zgrid = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(na, nb / 4) / 1024 + 1);
+    hipLaunchKernelGGL(k_ba_mode, dim3(zgrid), dim3(1024), 0, st, (const uint32_t *)a.f.bm, a.nwords4, a.record_policy,
+                       a.mode, a.cnt1, na, a.new_bits, nb);
     if (g_stage1_prefetch)
         hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, true>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
                            dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
@@ -1038,12 +1061,10 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
-    // one thread per new_bits word (32 keys): the per-thread chain of a smaller grid was the C1 add's third-largest cost
-    hipLaunchKernelGGL(k_ba_keys, dim3((unsigned)std::min<uint64_t>(2048, ((a.nchunk + 31) / 32 + 255) / 256)), dim3(256),
-                       0, st, a.ctr, a.nchunk, a.f.k,
-                       a.new_bits, a.overflow, a.mode);
-    hipLaunchKernelGGL(k_ba_final, dim3(grid_for_pc(a.nchunk)), dim3(256), 0, st, a.new_bits, a.nchunk, a.base,
-                       a.out_new, a.count, a.overflow);
+    // one thread per 32 keys (a per-thread chain over a smaller grid was the C1 add's third-largest cost)
+    hipLaunchKernelGGL(k_ba_final, dim3((unsigned)std::min<uint64_t>(2048, ((a.nchunk + 31) / 32 + 255) / 256)),
+                       dim3(256), 0, st, a.new_bits, a.ctr, a.f.k, a.nchunk, a.base, a.out_new, a.count, a.overflow,
+                       a.mode);
 }
 
 template <int KLEN>

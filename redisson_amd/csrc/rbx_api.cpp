@@ -382,8 +382,12 @@ static int new_bitmap(rbx_ctx *c, uint64_t size_bits, hipStream_t st, std::share
         HIP_TRY(hipMalloc(&b->d_words, bytes));
         HIP_TRY(hipMalloc(&b->d_len, sizeof(unsigned long long)));
     }
-    HIP_TRY(hipMemsetAsync(b->d_words, 0, bytes, st));
-    HIP_TRY(hipMemsetAsync(b->d_len, 0, sizeof(unsigned long long), st));
+    if (b->pool) {  // the words and the length word's 256-byte tail: one fill
+        HIP_TRY(hipMemsetAsync(b->d_words, 0, bytes + 256, st));
+    } else {
+        HIP_TRY(hipMemsetAsync(b->d_words, 0, bytes, st));
+        HIP_TRY(hipMemsetAsync(b->d_len, 0, sizeof(unsigned long long), st));
+    }
     b->cap_bytes = bytes;
     c->ks.generation++;
     *out = b;
@@ -627,7 +631,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     RBX_TRY(c->pa_cnt.reserve(ncnt * 4));
     const uint64_t nbw = (uint64_t)nranges << (kBaKeyRangeBits - 5);  // whole ranges (the records kernel's images)
     RBX_TRY(c->pa_bits.reserve(nbw * 4));
-    // per-key non-owner counters (one byte per key; k_ba_keys zeroes what it read): zeroed once
+    // per-key non-owner counters (one byte per key; k_ba_final zeroes what it read): zeroed once
     // when (re)allocated
     if (c->pa_ctr.cap < nbw * 32) {
         RBX_TRY(c->pa_ctr.reserve(nbw * 32));
@@ -671,8 +675,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
             }
             a.stamps = c->pa_stamps.as<unsigned long long>();
         }
-        HIP_TRY(hipMemsetAsync(a.cnt1, 0, ncnt * 4, st));
-        HIP_TRY(hipMemsetAsync(a.new_bits, 0, (uint64_t)a.nranges << (kBaKeyRangeBits - 5) << 2, st));
+        // the counters (but the mode word) and new_bits are zeroed by k_ba_mode, the chunk's first kernel
         launch_add_partitioned_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
         uint32_t ovf = 0;

@@ -30,7 +30,7 @@ import re
 SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_bk_probe", r"k_bk_probe"),
          ("k_bk_misses", r"k_bk_misses"), ("k_bk_final", r"k_bk_final"), ("k_stream_compact", r"k_stream_compact"),
          ("k_ba_stage1", r"k_ba_stage1<"), ("k_ba_rebucket", r"k_ba_rebucket"), ("k_ba_region", r"k_ba_region"),
-         ("k_ba_keys", r"k_ba_keys"), ("k_ba_final", r"k_ba_final"),
+         ("k_ba_keys_rec", r"k_ba_keys_rec"), ("k_ba_keys", r"k_ba_keys\("), ("k_ba_mode", r"k_ba_mode"), ("k_ba_final", r"k_ba_final"),
          ("k_stream_probe", r"k_stream_probe<"), ("k_stream_probe8", r"k_stream_probe8<"),
          ("k_stream_walk", r"k_stream_walk"), ("k_stream_final8", r"k_stream_final8<"),
          ("k_stream_final", r"k_stream_final\("), ("k_madd_probe8", r"k_madd_probe8<"),
@@ -141,7 +141,8 @@ def main():
     # one API call = these kernels in sequence, possibly once per chunk: per-call totals =
     # all profiled launches' counters / the calls in the profiled run (--calls)
     for name, parts in (("contains_pipeline", ("k_bk_stage1", "k_bk_emit2", "k_bk_probe", "k_bk_misses", "k_bk_final")),
-                        ("add_pipeline", ("k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys", "k_ba_final")),
+                        ("add_pipeline", ("k_ba_mode", "k_ba_stage1", "k_ba_rebucket", "k_ba_region", "k_ba_keys",
+                                          "k_ba_keys_rec", "k_ba_final")),
                         ("stream_pipeline", ("k_stream_compact", "k_stream_probe", "k_stream_probe8", "k_stream_contains",
                                              "k_stream_contains_q", "k_stream_commit", "k_stream_final8",
                                              "k_stream_walk", "k_stream_final")),
