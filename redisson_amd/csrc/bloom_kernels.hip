@@ -696,9 +696,17 @@ __global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restric
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t t0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
     uint32_t bits = 0;
+    if (t0 + 16 <= nchunk && ((base + t0) & 15) == 0) {  // the lane's 16 op bytes in one load (r05)
+        using u8x16v = uint8_t __attribute__((ext_vector_type(16)));
+        const u8x16v v = *(const u8x16v *)(op + base + t0);
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-        if (t0 + q < nchunk && op[base + t0 + q]) bits |= 1u << q;
+        for (int q = 0; q < 16; ++q)
+            if (v[q]) bits |= 1u << q;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (t0 + q < nchunk && op[base + t0 + q]) bits |= 1u << q;
+    }
     const uint32_t c = (uint32_t)__popc(bits);
     uint32_t x = c;  // inclusive scan over the wave
 #pragma unroll
