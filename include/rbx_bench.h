@@ -75,6 +75,10 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           optimistic SETBITs (returning atomicOr) with a small conflict table for the
  *                           zero bits two keys share, 1 the 8-byte first-setter table (claims by one CAS,
  *                           replies from the first claim's slot, walk commit), 0 the 16-byte epoch table
+ *   "add_multi_segment"     1 (default): a multi-tenant add whose filters are all distinct runs each
+ *                           segment of <= add_multi_segmax keys (default 16384) in one workgroup (LDS
+ *                           first setters, plain word stores), longer ones on the path above; 0: off
+ *   "add_multi_segmax"      that segment-length limit (keys, >= 1)
  *   "add_multi_conflict_log2"  entries (log2, 6..24, default 17) of the conflict table of mode 2; past
  *                           half full the chunk's replies come from the full first-setter table
  *   "walk_reset_all"        the 8-byte table's walk: bit 0 (ordered stream) / bit 1 (multi-tenant add)

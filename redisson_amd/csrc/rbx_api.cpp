@@ -190,7 +190,8 @@ struct rbx_ctx {
     DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
     DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
     DevBuf st_fslot;             // ordered stream (r05): per add, the slot of its first zero bit's claim
-    DevBuf madd_c;               // multi-tenant add (r05): conflict table C + its MaddxState
+    DevBuf madd_c;               // multi-tenant add (r05): conflict table C + its MaddxState (+ the `big` flag)
+    uint64_t madd_maxseg_hint = ~0ULL;  // set by the host-arena add_multi: its largest segment (keys)
     uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
     uint64_t st_geom[4] = {0, 0, 0, 0};             // last stream call: bb, fbits, pb, chunk
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
@@ -1605,13 +1606,19 @@ static int g_add_multi_t8 = 2;
 // rbx_tune("add_multi_conflict_log2"): entries of the conflict table C, log2 (default 17: 1 MiB, L2-
 // resident; tests use small ones to run the overflow path)
 static uint32_t g_maddx_lgc = 17;
+// rbx_tune("add_multi_segment"): 1 (default) a batch whose filters are all distinct runs its segments of
+// <= add_multi_segmax keys one workgroup each (k_madd_seg: LDS first setters, plain word stores, no
+// memory-side atomics), longer segments on the chunked path; 0 everything on the chunked path
+static int g_madd_seg = 1;
+static uint64_t g_madd_segmax = 16384;
 
 // Multi-tenant add on the 8-byte table: chunks of <= min(2^pb - 1, 2^27 / k) keys, each probe ->
 // final -> walk, in key order (a chunk's bits are set before the next probes).  The table and its
 // EMPTY state are shared with the ordered stream (st_t8 / st_t8_entries).
 static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg_off, uint32_t nseg,
                           uint32_t kmax, uint32_t bb, uint32_t pb, uint8_t *d_out_new,
-                          unsigned long long *d_seg_counts, hipStream_t st) {
+                          unsigned long long *d_seg_counts, hipStream_t st, const uint32_t *big = nullptr,
+                          uint64_t segmax = 0) {
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     const uint64_t cap = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, (1ULL << 27) / k);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, cap));
@@ -1659,6 +1666,8 @@ static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg
             a.c8 = c->madd_c.as<unsigned long long>();
             a.lgC = g_maddx_lgc;
             a.cst = (MaddxState *)(a.c8 + (1ULL << g_maddx_lgc));
+            a.big = big;
+            a.segmax = segmax;
         }
         launch_madd8_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
@@ -1685,6 +1694,30 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     uint32_t bb = 1, fbits = 0;
     while ((1ULL << bb) < c->filt_maxbits) ++bb;
     while ((1ULL << fbits) < c->filt_nfids) ++fbits;
+    if (g_add_multi_t8 == 2 && g_madd_seg && kmax <= 16 && c->filt_nfids == nseg && bb + fbits <= 41) {
+        // every filter in one segment only: k_madd_seg, one workgroup per segment; the chunked path
+        // then handles only segments past segmax (and returns at once when there are none)
+        RBX_TRY(c->madd_c.reserve((8ULL << g_maddx_lgc) + 64));
+        uint32_t *big = (uint32_t *)(c->madd_c.as<unsigned long long>() + (1ULL << g_maddx_lgc)) + 4;
+        HIP_TRY(hipMemsetAsync(big, 0, 4, st));
+        MaddSegArgs a{};
+        a.keys = k;
+        a.filt = c->filt_table.as<FilterDesc>();
+        a.seg_off = d_seg_offsets;
+        a.nseg = nseg;
+        a.kmax = kmax;
+        a.lgs = 12;  // 4096 slots per table, 64 KiB of LDS: two workgroups per CU
+        a.tile = std::max<uint32_t>(64, std::min<uint32_t>(256, (2048 / std::max<uint32_t>(kmax, 1)) & ~63u));
+        a.segmax = g_madd_segmax;
+        a.out_new = d_out_new;
+        a.seg_counts = d_counts;
+        a.big = big;
+        launch_madd_seg(a, fast_len(k), st);
+        HIP_TRY(hipGetLastError());
+        if (c->madd_maxseg_hint <= g_madd_segmax) return RBX_OK;  // host-known: no long segment
+        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, big,
+                              g_madd_segmax);
+    }
     if (g_add_multi_t8 && kmax <= 32 && bb + fbits <= 41)
         return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st);
     FilterDesc dummy{};
@@ -1898,7 +1931,15 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
         d_out = c->out_bytes.as<uint8_t>();
     }
     rbx_keys kd{dk.bytes, dk.offsets, dk.stride, dk.n};
-    if (is_add) RBX_TRY(rbx_bloom_add_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts, c->stream));
+    if (is_add) {
+        uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
+        for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
+        c->madd_maxseg_hint = mx;
+        const int rc = rbx_bloom_add_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts,
+                                               c->stream);
+        c->madd_maxseg_hint = ~0ULL;
+        RBX_TRY(rc);
+    }
     else RBX_TRY(rbx_bloom_contains_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts, c->stream));
     if (out_flags) HIP_TRY(hipMemcpyAsync(out_flags, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
     std::vector<unsigned long long> cnt(nseg);
@@ -3352,6 +3393,16 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_multi_table8")) {
         if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0, 1 or 2");
         g_add_multi_t8 = value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_multi_segment")) {
+        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_segment: 0 or 1");
+        g_madd_seg = value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_multi_segmax")) {
+        if (value < 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_segmax >= 1");
+        g_madd_segmax = (uint64_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "add_multi_conflict_log2")) {

@@ -201,8 +201,27 @@ struct MaddChunkArgs {
     unsigned long long *c8;
     uint32_t lgC;
     MaddxState *cst;
+    // r05 per-segment path (k_madd_seg) in front: non-null = every k_maddx_* kernel returns unless *big
+    // (a segment past segmax exists), and handles only the keys of such segments
+    const uint32_t *big;
+    uint64_t segmax;
 };
 void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st);
+// r05 per-segment multi-tenant add (stream_kernels.hip k_madd_seg): one workgroup per segment, every
+// filter of the batch in one segment only (disjoint bitmaps), k <= 16; segments past segmax keys set
+// *big and are left to the k_maddx_* chunks
+struct MaddSegArgs {
+    KeysDev keys;
+    const FilterDesc *filt;
+    const uint64_t *seg_off;
+    uint32_t nseg, kmax;
+    uint32_t lgs, tile;       // LDS tables of 2^lgs slots; keys per tile (<= 256)
+    uint64_t segmax;
+    uint8_t *out_new;
+    unsigned long long *seg_counts;
+    uint32_t *big;            // zeroed before the launch
+};
+void launch_madd_seg(const MaddSegArgs &a, int klen_fast, hipStream_t st);
 // entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)
 __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
     const uint64_t need = (uint64_t)nadds * kmax;

@@ -812,14 +812,21 @@ __global__ __launch_bounds__(256) void k_maddx_gather(KeysDev keys, uint64_t bas
                                                       const uint64_t *__restrict__ seg_off, uint32_t nseg,
                                                       const uint32_t *__restrict__ tile_seg0,
                                                       uint32_t *__restrict__ zmask, unsigned long long *__restrict__ C,
-                                                      uint32_t lgC, MaddxState *__restrict__ cst) {
+                                                      uint32_t lgC, MaddxState *__restrict__ cst,
+                                                      const uint32_t *__restrict__ big, uint64_t segmax) {
+    if (big && !*big) return;  // k_madd_seg took every segment (uniform; K2..K5 check the same word)
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t s = tid; s < (1ULL << lgC); s += stride) C[s] = ~0ULL;  // the previous chunk's C
     if (tid == 0) *cst = MaddxState{0, 0};
     for (uint64_t t = tid; t < nchunk; t += stride) {
         const uint64_t i = base + t;
-        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
+        const uint32_t sg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
+        if (big && seg_off[sg + 1] - seg_off[sg] <= segmax) {  // k_madd_seg's segment: not here
+            zmask[t] = 0;
+            continue;
+        }
+        const FilterDesc f = filt[sg];
         uint64_t h1, h2;
         hash_key<KLEN>(keys, i, h1, h2);
         uint32_t word[KMAX], idxs[KMAX];
@@ -851,7 +858,9 @@ __global__ __launch_bounds__(256) void k_maddx_set(KeysDev keys, uint64_t base, 
                                                    const uint32_t *__restrict__ tile_seg0,
                                                    const uint32_t *__restrict__ zmask,
                                                    unsigned long long *__restrict__ C, uint32_t lgC, uint32_t bb,
-                                                   uint32_t pb, MaddxState *__restrict__ cst) {
+                                                   uint32_t pb, MaddxState *__restrict__ cst,
+                                                   const uint32_t *__restrict__ big) {
+    if (big && !*big) return;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t cmask = (1ULL << lgC) - 1;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
@@ -899,7 +908,9 @@ __global__ __launch_bounds__(256) void k_maddx_claim(KeysDev keys, uint64_t base
                                                      const uint32_t *__restrict__ zmask,
                                                      unsigned long long *__restrict__ C, uint32_t lgC,
                                                      unsigned long long *__restrict__ T, uint32_t lgT, uint32_t bb,
-                                                     uint32_t pb, const MaddxState *__restrict__ cst, uint32_t batch) {
+                                                     uint32_t pb, const MaddxState *__restrict__ cst, uint32_t batch,
+                                                     const uint32_t *__restrict__ big) {
+    if (big && !*big) return;
     const MaddxState cs = *cst;
     if (cs.count == 0 && !cs.overflow) return;  // no shared zero bit: every key with one is new
     const uint64_t pmask = (1ULL << pb) - 1;
@@ -938,18 +949,23 @@ __global__ __launch_bounds__(256) void k_maddx_reply(KeysDev keys, uint64_t base
                                                      const unsigned long long *__restrict__ T, uint32_t lgT,
                                                      uint32_t bb, uint32_t pb, const MaddxState *__restrict__ cst,
                                                      uint8_t *__restrict__ out_new,
-                                                     unsigned long long *__restrict__ seg_counts) {
+                                                     unsigned long long *__restrict__ seg_counts,
+                                                     const uint32_t *__restrict__ big, uint64_t segmax) {
+    if (big && !*big) return;
     const MaddxState cs = *cst;
     const uint64_t pmask = (1ULL << pb) - 1;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t n_up = (nchunk + 63) & ~63ULL;  // whole waves (wave_seg_add)
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_up; t += stride) {
-        const bool in = t < nchunk;
         const uint64_t i = base + t;
         uint32_t seg = 0;
-        bool isnew = false;
+        bool in = t < nchunk;
         if (in) {
             seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
+            in = !(big && seg_off[seg + 1] - seg_off[seg] <= segmax);  // k_madd_seg answered it
+        }
+        bool isnew = false;
+        if (in) {
             const uint32_t zm = zmask[t];
             if (zm && cs.count == 0 && !cs.overflow) {
                 isnew = true;
@@ -979,11 +995,168 @@ __global__ __launch_bounds__(256) void k_maddx_reply(KeysDev keys, uint64_t base
 
 // after an overflowed chunk: T back to EMPTY (its bits were set by k_maddx_set already)
 __global__ __launch_bounds__(256) void k_maddx_reset(unsigned long long *__restrict__ T, uint32_t lgT,
-                                                     const MaddxState *__restrict__ cst) {
+                                                     const MaddxState *__restrict__ cst, const uint32_t *__restrict__ big) {
+    if (big && !*big) return;
     if (!cst->overflow) return;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < (1ULL << lgT); s += stride)
         if (T[s] != ~0ULL) T[s] = ~0ULL;
+}
+
+// ---- multi-tenant add, r05: one workgroup per segment ------------------------------------------
+// When every filter of an add batch appears in one segment only, the segments touch disjoint bitmaps,
+// so a workgroup that owns a segment owns its bitmap for the whole call: no other workgroup reads or
+// writes it, and no memory-side atomic is needed.  The workgroup walks its segment in tiles of TILE
+// keys (one per thread): (1) every key's k words are read -- `sc1` loads, served by this XCD's L2,
+// which holds the previous tile's stores (the vector L1 is not refreshed by stores); (2) its zero bits
+// go into two LDS hash tables: bit -> smallest position of a key meeting it at 0 (CAS + min), word ->
+// the OR of the zero bits and the word as read (every key reads the same value: no store of this tile
+// has happened yet); (3) every word is written back once with a plain store, old | bits; (4) key t is
+// new iff one of its zero bits has t as smallest position.  Tiles run one after another (each sees the
+// previous one's bits), so a key is new iff one of its bits was 0 before the batch and no earlier key
+// of the batch touches it: M/RedissonBloomFilter.java:104-137 in CommandBatchService order.  Segments
+// longer than segmax keys are left to the k_maddx_* chunks (flag `big`).
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(256) void k_madd_seg(KeysDev keys, const FilterDesc *__restrict__ filt,
+                                                  const uint64_t *__restrict__ seg_off, uint32_t nseg, uint32_t lgs,
+                                                  uint32_t tile, uint64_t segmax, uint8_t *__restrict__ out_new,
+                                                  unsigned long long *__restrict__ seg_counts,
+                                                  uint32_t *__restrict__ big) {
+    extern __shared__ unsigned long long s_dyn[];
+    const uint32_t S = 1u << lgs, smask = S - 1u;
+    unsigned long long *BT = s_dyn;              // bit << 32 | smallest position in the segment; ~0 empty
+    uint32_t *WK = (uint32_t *)(BT + S);         // word index; ~0 empty
+    uint32_t *WV = WK + S;                       // old word | zero bits
+    __shared__ uint32_t s_red[8];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint32_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const uint64_t a = seg_off[sg], b = seg_off[sg + 1];
+        if (b - a > segmax) {  // uniform: left to the chunked path
+            if (tid == 0) atomicOr(big, 1u);
+            continue;
+        }
+        if (b == a) continue;
+        const FilterDesc f = filt[sg];
+        uint32_t maxidx = 0, nnew = 0;
+        for (uint64_t base = a; base < b; base += tile) {
+            for (uint32_t q = tid; q < S; q += blockDim.x) {
+                BT[q] = ~0ULL;
+                WK[q] = ~0u;
+                WV[q] = 0u;
+            }
+            __syncthreads();
+            const uint64_t i = base + tid;
+            const bool act = tid < tile && i < b;
+            const uint32_t pos = (uint32_t)(i - a);
+            uint32_t idxs[KMAX], word[KMAX], zm = 0;
+            if (act) {
+                uint64_t h1, h2;
+                hash_key<KLEN>(keys, i, h1, h2);
+                uint64_t h = h1;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if ((uint32_t)j < f.k) {
+                        const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+                        idxs[j] = idx;
+                        word[j] = __hip_atomic_load(&f.bm[idx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        maxidx = idx > maxidx ? idx : maxidx;
+                    }
+                    h += (j & 1) ? h1 : h2;
+                }
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j)
+                    if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (!((zm >> j) & 1u)) continue;
+                    const unsigned long long mine = ((unsigned long long)idxs[j] << 32) | pos;
+                    for (uint32_t q = (idxs[j] * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
+                        const unsigned long long o = atomicCAS(&BT[q], ~0ULL, mine);
+                        if (o == ~0ULL) break;
+                        if ((uint32_t)(o >> 32) == idxs[j]) {
+                            if (o > mine) atomicMin(&BT[q], mine);
+                            break;
+                        }
+                    }
+                    const uint32_t w = idxs[j] >> 5;
+                    for (uint32_t q = (w * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
+                        const uint32_t o = atomicCAS(&WK[q], ~0u, w);
+                        if (o == ~0u || o == w) {
+                            atomicOr(&WV[q], word[j] | bit_in_word(idxs[j]));
+                            break;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            for (uint32_t q = tid; q < S; q += blockDim.x) {  // every touched word once, plain stores
+                const uint32_t w = WK[q];
+                if (w != ~0u) f.bm[w] = WV[q];
+            }
+            bool isnew = false;
+            if (act) {
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (!((zm >> j) & 1u) || isnew) continue;
+                    for (uint32_t q = (idxs[j] * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
+                        const unsigned long long o = BT[q];
+                        if ((uint32_t)(o >> 32) == idxs[j]) {
+                            isnew = (uint32_t)o == pos;
+                            break;
+                        }
+                    }
+                }
+                if (out_new) out_new[i] = isnew;
+            }
+            nnew += isnew;
+            // this tile's stores reach L2 before the next tile's sc1 loads, and the tables are reused
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        // the segment's count and the Redis string length (every SETBIT grows it to idx / 8 + 1)
+        uint32_t c = nnew, mx = maxidx;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            c += __shfl_down(c, off, 64);
+            mx = max(mx, (uint32_t)__shfl_down(mx, off, 64));
+        }
+        if (lane == 0) {
+            s_red[wave] = c;
+            s_red[4 + wave] = mx;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tc = 0, tm = 0;
+            for (uint32_t w = 0; w < blockDim.x / 64u; ++w) {
+                tc += s_red[w];
+                tm = max(tm, s_red[4 + w]);
+            }
+            if (tc && seg_counts) atomicAdd(&seg_counts[sg], (unsigned long long)tc);
+            raise_redis_len(f.redis_len, (unsigned long long)(tm >> 3) + 1ULL);
+        }
+        __syncthreads();  // s_red reuse
+    }
+}
+
+template <int KLEN>
+static void launch_madd_seg_len(const MaddSegArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)(8 + 4 + 4) << a.lgs;
+    const dim3 grid(std::min<uint32_t>(a.nseg, 4096));
+    if (a.kmax <= 8)
+        hipLaunchKernelGGL((k_madd_seg<KLEN, 8>), grid, dim3(256), lds, st, a.keys, a.filt, a.seg_off, a.nseg, a.lgs,
+                           a.tile, a.segmax, a.out_new, a.seg_counts, a.big);
+    else
+        hipLaunchKernelGGL((k_madd_seg<KLEN, 16>), grid, dim3(256), lds, st, a.keys, a.filt, a.seg_off, a.nseg, a.lgs,
+                           a.tile, a.segmax, a.out_new, a.seg_counts, a.big);
+}
+
+void launch_madd_seg(const MaddSegArgs &a, int klen_fast, hipStream_t st) {
+    switch (klen_fast) {
+    case 16: launch_madd_seg_len<16>(a, st); break;
+    case 32: launch_madd_seg_len<32>(a, st); break;
+    case 64: launch_madd_seg_len<64>(a, st); break;
+    default: launch_madd_seg_len<0>(a, st); break;
+    }
 }
 
 static int g_stream_slots = 1;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel (default)
@@ -1087,16 +1260,16 @@ template <int KLEN, int KMAX>
 static void launch_maddx_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(std::max<uint64_t>(a.nchunk, 1ULL << a.lgC), kMaxGrid);
     hipLaunchKernelGGL((k_maddx_gather<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.cst);
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.cst, a.big, a.segmax);
     hipLaunchKernelGGL((k_maddx_set<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.bb, a.pb, a.cst);
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.bb, a.pb, a.cst, a.big);
     hipLaunchKernelGGL((k_maddx_claim<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
                        a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst,
-                       g_probe8_batch);
+                       g_probe8_batch, a.big);
     hipLaunchKernelGGL((k_maddx_reply<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
                        a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst, a.out_new,
-                       a.seg_counts);
-    hipLaunchKernelGGL(k_maddx_reset, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.lg, a.cst);
+                       a.seg_counts, a.big, a.segmax);
+    hipLaunchKernelGGL(k_maddx_reset, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.lg, a.cst, a.big);
 }
 
 template <int KLEN>

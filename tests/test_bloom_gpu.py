@@ -384,6 +384,107 @@ def test_multi_tenant_add_first_setter_tables(client, fresh, table8, clog2, chun
 ADD_MULTI_DEFAULT = 2
 
 
+@pytest.mark.parametrize("segmax", [16384, 300, 1])
+@pytest.mark.parametrize("fixed", [True, False])
+def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
+    """r05: a multi-tenant add whose filters are all distinct runs one workgroup per segment (k_madd_seg:
+    LDS first setters, plain word stores, tiles of <= 256 keys in order); segments longer than
+    add_multi_segmax keys go to the chunked path in the same call (segmax 300: both paths; 1: every
+    non-trivial segment chunked).  40 filters with k = 3..16 (KMAX 8 and 16), 0..1,500 keys per segment
+    (empty segments, many tiles per segment), keys repeated within a segment and across tile boundaries
+    (shared zero bits), fixed 16-byte or variable-length keys.  Per-key flags, per-segment counts and every
+    bitmap vs the oracle; then the same batch again (every key already present)."""
+    rng = np.random.default_rng(1300 + segmax + int(fixed))
+    nt = 40
+    names = [f"{fresh}-{t}" for t in range(nt)]
+    refs = []
+    for t, n in enumerate(names):
+        m, k = int(rng.integers(2_000, 400_000)), int(rng.integers(3, 17))
+        client.getBloomFilter(n).tryInitRaw(m, k)
+        refs.append(O.OracleBloom(m, k))
+    handles = [BloomHandle(client, n) for n in names]
+    sizes = [int(x) for x in rng.integers(0, 1500, size=nt)]
+    sizes[3] = 0
+    segs = np.zeros(nt + 1, np.uint64)
+    segs[1:] = np.cumsum(sizes)
+    n = int(segs[-1])
+    if fixed:
+        pool = rng.integers(0, 256, size=(max(1, n // 3), 16), dtype=np.uint8)
+        mat = pool[rng.integers(0, len(pool), size=n)]
+        keys, arena, sub = mat, Arena.fixed(mat), (lambda a, b: O.fixed_arena(mat[a:b]))
+    else:
+        pool = [rng.bytes(int(L)) for L in rng.integers(0, 40, size=max(1, n // 3))]
+        keys = [pool[int(j)] for j in rng.integers(0, len(pool), size=n)]
+        arena, sub = Arena(keys), (lambda a, b: O.arena(keys[a:b]))
+    assert L.lib().rbx_tune(b"add_multi_segmax", segmax) == 0
+    try:
+        for rep in range(2):
+            counts, flags = bloom_add_multi(client, handles, segs, arena, per_key=True)
+            for t in range(nt):
+                a, b = int(segs[t]), int(segs[t + 1])
+                c, fl = refs[t].add(*sub(a, b), per_key=True)
+                assert counts[t] == c and np.array_equal(flags[a:b], fl), (rep, t, sizes[t])
+            if rep == 0:
+                assert int(counts.sum()) > n // 4
+    finally:
+        L.lib().rbx_tune(b"add_multi_segmax", 16384)
+    for nm, r in zip(names, refs):
+        assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
+    for h in handles:
+        h.close()
+    for nm in names:
+        client.getBloomFilter(nm).delete()
+
+
+@pytest.mark.parametrize("segment", [1, 0])
+def test_multi_tenant_add_segment_path_at_c3_shape(client, fresh, segment):
+    """The bench's C3 add shape at 20,000 tenants (tryInit(1e6, 1e-3): 14,377,587 bits, k = 10) at design
+    fill: one add_multi of 1,000 fresh 16-byte keys per tenant, on the per-segment path (1) and on the
+    chunked optimistic path (0); per-key flags and counts vs the oracle for 300 sampled tenants, every
+    count checked against the flags."""
+    import torch
+
+    nt, per = 20_000, 1000
+    rng = np.random.default_rng(0xC3ADD + segment)
+    pool = rng.integers(0, 256, size=16 << 20, dtype=np.uint8)
+    dpool = torch.from_numpy(pool).cuda()
+    names = [f"{fresh}:{t:05d}" for t in range(nt)]
+    offs = np.zeros(nt, np.int64)
+    handles = []
+    nb = (14_377_587 + 7) // 8
+    try:
+        for t, nm in enumerate(names):
+            assert client.getBloomFilter(nm).tryInit(1_000_000, 1e-3)
+            offs[t] = int(rng.integers(0, (pool.size - nb) // 256)) * 256
+            assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), dpool.data_ptr() + int(offs[t]), nb,
+                                                None) == 0
+            handles.append(BloomHandle(client, nm))
+        keys = rng.integers(0, 256, size=(nt * per, 16), dtype=np.uint8)
+        seg = np.arange(nt + 1, dtype=np.uint64) * np.uint64(per)
+        assert L.lib().rbx_tune(b"add_multi_segment", segment) == 0
+        try:
+            counts, flags = bloom_add_multi(client, handles, seg, Arena.fixed(keys), per_key=True)
+        finally:
+            L.lib().rbx_tune(b"add_multi_segment", 1)
+        sample = rng.choice(nt, size=300, replace=False)
+        for t in sample:
+            t = int(t)
+            r = O.OracleBloom(14_377_587, 10)
+            r.bitmap[:nb] = pool[offs[t]:offs[t] + nb]
+            r.redis_len = nb
+            c, fl = r.add(*O.fixed_arena(keys[t * per:(t + 1) * per]), per_key=True)
+            assert counts[t] == c and np.array_equal(flags[t * per:(t + 1) * per], fl), t
+            assert client.getBloomFilter(names[t]).exportBitmap() == r.redis_string(), t
+        assert int(counts.sum()) == int(flags.sum()) and int(counts.sum()) > nt * per * 0.99
+    finally:
+        for h in handles:
+            h.close()
+        for nm in names:
+            client.getBloomFilter(nm).delete()
+        del dpool
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("table8", [2, 1, 0])
 def test_multi_tenant_add_filter_ids_past_2_17(client, fresh, table8):
     """per-key add parity of a multi-tenant add batch whose filter ids reach 2^17:
