@@ -789,16 +789,20 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
     # a key + k x 8 B gathered + k x 8 B RMW
     algo = n * (16 + 2 * k * 8)
     tj = args.traffic_json if (args.keys, args.tenants, world) == (100_000_000, 100_000, 1) else None
-    mode = dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv).get("add_multi_table8", "2")
-    pipe = {"1": "madd_pipeline", "0": None}.get(mode, "maddx_pipeline")
+    tune = dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv)
+    mode, seg_path = tune.get("add_multi_table8", "2"), tune.get("add_multi_segment", "1") != "0"
+    if mode == "2" and seg_path:  # every tenant of the batch distinct: one workgroup per segment
+        pipe, path = "k_madd_seg", "one workgroup per segment (k_madd_seg: LDS first setters, plain word stores)"
+    else:
+        pipe = {"1": "madd_pipeline", "0": None}.get(mode, "maddx_pipeline")
+        path = {"0": "16-byte epoch table (k_bloom_add_probe + commit)",
+                "1": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"}.get(
+                    mode, "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)")
     del keys
     return {"metric": "Bloom add keys/sec (whole node), C3 tenants: one add(Collection) per tenant",
             "value": sum_over_ranks(world, n) / step_s, "unit": "keys/s", "ms_per_step": step_s * 1e3,
             "keys_per_gpu": n, "new_keys_per_step": new, "steps": steps, "warmup": warmup,
-            "path": {"0": "16-byte epoch table (k_bloom_add_probe + commit)",
-                     "1": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"}.get(
-                         dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv).get("add_multi_table8", "2"),
-                         "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)"),
+            "path": path,
             "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
                          "traffic": load_traffic(tj, pipe, "hbm_bytes_by_class") if pipe else None,

@@ -12,7 +12,7 @@ RBX_STREAM_BYTES="k_bk_stage1=3.2e9 k_bloom_contains=3.2e9" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c2" --workload c2 || exit 1
 fi
 if [[ ",$ONLY," == *",c3,"* ]]; then
-RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9 k_maddx_gather=1.333e8 k_madd_probe8=1.333e8" \
+RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9 k_maddx_gather=1.333e8 k_madd_probe8=1.333e8 k_madd_seg=1.6e9" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c3" --workload c3 || exit 1
 fi
 [[ ",$ONLY," == *",c4,"* ]] && { timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c4" --workload c4 || exit 1 ; }
