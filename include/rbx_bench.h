@@ -57,6 +57,9 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           region-pass phase times, read by rbx_bench_add_stamps)
  *   "add_region_kernel"     partitioned add region pass: 2 (default: 6-byte region pairs,
  *                           pipelined k_ba_region6), 1 (8-byte pairs, k_ba_region)
+ *   "add_rebucket_lines"    partitioned add rebucket: 0 (default) k_ba_rebucket, 1 k_ba_emit2
+ *                           (whole-line region runs, LDS carries; measured 0.03 ms slower at C2),
+ *                           2 k_ba_emit2 when a chunk has >= 1024 stage-1 partitions
  *   "add_rec_lds_limit"     owner records a region block stages in LDS, 0..7168 (default 7168;
  *                           tests use small limits to run the direct-report fallback)
  *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,

@@ -321,6 +321,156 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
     ps.flush(stamps);
 }
 
+// B' (r05) ------------------------------------------------------------------------------
+// The rebucket with whole-line runs (the shape of contains_partitioned.hip's k_bk_emit2): one block
+// per stage-1 partition, its tiles in order, every run a multiple of kBaLine pairs (two 64-byte lines
+// of lo words + one of hi halves), each fine bucket's remainder carried in LDS (6-byte form) to the
+// next tile, and a partition's last remainders padded to a whole line with kBaPadHi pairs, which the
+// region pass skips.  k_ba_rebucket's runs start and end mid-line: ~12M of its 45M write requests at
+// C2 are partial lines (profiles/r04/r04p_c2), and a partial line costs a whole request.  Few
+// partitions (C1: 48) would leave most CUs idle, so the launcher keeps k_ba_rebucket there.
+constexpr uint32_t kBaLine = 32;
+constexpr uint16_t kBaPadHi = 0xffffu;  // hi half of a padding pair: real keys are < 2^26 (hi < 1024)
+static_assert(kBaMaxRegionPairs <= 65536, "region pair counts fit the LDS counters");
+
+template <int PER, bool STAMP>
+__global__ __launch_bounds__(1024) void k_ba_emit2(const unsigned long long *__restrict__ pin,
+                                                   const uint32_t *__restrict__ cnt_in, uint64_t cap_in,
+                                                   uint32_t nparents, uint32_t sub_div, uint32_t shift_out, uint32_t fo,
+                                                   uint32_t nparts_out, unsigned long long *__restrict__ pout,
+                                                   uint32_t *__restrict__ cnt_out, uint64_t cap_out,
+                                                   uint32_t *__restrict__ overflow, unsigned long long *__restrict__ stamps) {
+    constexpr uint32_t NT = 1024, TILE = 2 * PER * NT;
+    PhaseStamps<STAMP, 4> ps;
+    ps.start();
+    __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
+    __shared__ uint32_t s_clo[256 * kBaLine];  // carried pairs: lo words
+    __shared__ uint16_t s_chi[256 * kBaLine];  // and hi halves
+    __shared__ uint32_t s_cnt2[2][256], s_start[256], s_pos[256], s_gb[256], s_full[256], s_cn[256];
+    const uint32_t nf = 1u << fo, fmask = nf - 1;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nparts = nparents * sub_div;
+    auto lo_of = [](unsigned long long e) { return (uint32_t)(e >> 32) << 16 | ((uint32_t)e & 0xffffu); };
+    auto hi_of = [](unsigned long long e) { return (uint16_t)((uint32_t)e >> 16); };
+    // pair t of region r's run (whole lines: gb and every reservation are multiples of kBaLine)
+    auto put = [&](uint32_t r, uint64_t slot, uint32_t lo, uint16_t hi) {
+        if (slot < cap_out) {
+            uint32_t *plo = (uint32_t *)pout + (uint64_t)r * (cap_out * 3 / 2);
+            run_store(lo, plo + slot);
+            run_store(hi, (uint16_t *)(plo + cap_out) + slot);
+        } else {
+            *overflow = 1u;
+        }
+    };
+    for (uint32_t item = blockIdx.x; item < nparts; item += gridDim.x) {
+        // items parent-minor: the blocks running at one time reserve from different parents' regions
+        const uint32_t parent = item % nparents, part = parent * sub_div + item / nparents;
+        const uint64_t nc = min<uint64_t>(cnt_in[part], cap_in);
+        if (threadIdx.x < 256) {
+            s_cn[threadIdx.x] = 0;
+            s_cnt2[0][threadIdx.x] = 0;
+        }
+        uint32_t par = 0;
+        __syncthreads();
+        // cap_in is a multiple of 8192 pairs and TILE of 2048: every tile is 16-byte aligned
+        const u32x4 *src0 = (const u32x4 *)(pin + (uint64_t)part * cap_in);
+        u32x4 v[PER];  // the next tile, loaded while the current one is bucketed and written
+        auto load = [&](uint64_t st) {
+            const uint32_t mm = (uint32_t)min<uint64_t>(TILE, nc - st);
+#pragma unroll
+            for (int p = 0; p < PER; ++p) {
+                v[p] = u32x4{0u, 0u, 0u, 0u};
+                if (2 * (p * NT + threadIdx.x) < mm) v[p] = __builtin_nontemporal_load(src0 + st / 2 + p * NT + threadIdx.x);
+            }
+        };
+        if (nc) load(0);
+        for (uint64_t start = 0; start < nc; start += TILE) {
+            const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
+            uint32_t *s_cnt = s_cnt2[par];
+            if (threadIdx.x < 256) s_cnt2[par ^ 1][threadIdx.x] = 0;  // the next tile's (after this tile's last barrier)
+            unsigned long long e[2 * PER];
+#pragma unroll
+            for (int p = 0; p < PER; ++p) {
+                e[2 * p] = w2(v[p].x, v[p].y);
+                e[2 * p + 1] = w2(v[p].z, v[p].w);
+            }
+#pragma unroll
+            for (int p = 0; p < 2 * PER; ++p) {
+                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+                if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u);
+            }
+            __syncthreads();
+            ps.mark(0);
+            // reservations issued here, their results stored after the placement (which hides the
+            // round trip); the next tile's loads follow them
+            uint32_t gb = 0;
+            if (threadIdx.x < 64) bk_scan256(s_cnt, nf, s_start, s_pos);
+            else if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) {
+                const uint32_t f = threadIdx.x - 256;
+                const uint32_t r = (parent << fo) + f;
+                const uint32_t full = (s_cn[f] + s_cnt[f]) & ~(kBaLine - 1);
+                s_full[f] = full;
+                if (full && r < nparts_out) gb = atomicAdd(&cnt_out[r], full);
+            }
+            if (start + TILE < nc) load(start + TILE);
+            __syncthreads();
+            ps.mark(1);
+#pragma unroll
+            for (int p = 0; p < 2 * PER; ++p) {
+                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
+                if (q < m) s_img[atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u)] = e[p];
+            }
+            if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) s_gb[threadIdx.x - 256] = gb;
+            __syncthreads();
+            ps.mark(2);
+            // a wave per fine bucket: its carries then its new pairs, the whole lines out, the rest carried
+            for (uint32_t f = wave; f < nf; f += NT / 64) {
+                const uint32_t n = s_cnt[f], cn = s_cn[f], full = s_full[f], st = s_start[f];
+                const uint32_t r = (parent << fo) + f;
+                for (uint32_t t = lane; t < full; t += 64) {
+                    uint32_t lo;
+                    uint16_t hi;
+                    if (t < cn) {
+                        lo = s_clo[f * kBaLine + t];
+                        hi = s_chi[f * kBaLine + t];
+                    } else {
+                        const unsigned long long x = s_img[st + t - cn];
+                        lo = lo_of(x);
+                        hi = hi_of(x);
+                    }
+                    put(r, (uint64_t)s_gb[f] + t, lo, hi);
+                }
+                // full > 0 means full >= kBaLine > cn: every old carry went out above
+                const uint32_t rem = cn + n - full, from = full ? full - cn : 0u, to = full ? 0u : cn;
+                for (uint32_t t = lane; t < rem - to; t += 64) {
+                    const unsigned long long x = s_img[st + from + t];
+                    s_clo[f * kBaLine + to + t] = lo_of(x);
+                    s_chi[f * kBaLine + to + t] = hi_of(x);
+                }
+                if (lane == 0) s_cn[f] = rem;
+            }
+            par ^= 1u;
+            __syncthreads();
+            ps.mark(3);
+        }
+        for (uint32_t f = wave; f < nf; f += NT / 64) {  // the item's last remainders, padded to a line
+            const uint32_t cn = s_cn[f];
+            if (cn == 0) continue;  // uniform over the wave
+            const uint32_t r = (parent << fo) + f;
+            uint32_t gb = 0;
+            if (lane == 0) gb = atomicAdd(&cnt_out[r], kBaLine);
+            gb = __shfl(gb, 0, 64);
+            if (lane < kBaLine) {
+                if (lane < cn) put(r, (uint64_t)gb + lane, s_clo[f * kBaLine + lane], s_chi[f * kBaLine + lane]);
+                else put(r, (uint64_t)gb + lane, 0u, kBaPadHi);
+            }
+        }
+        __syncthreads();  // s_cn / carries reused by the next item
+        ps.mark(3);
+    }
+    ps.flush(stamps);
+}
+
 // mode -----------------------------------------------------------------------------------
 // Sampled fill of the bitmap -> how C reports new keys (see the header): 1 = non-owner counters,
 // 2 = owner records, 0 = owner bits.
@@ -714,7 +864,10 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (uint32_t p = 0; p < PER; p += 2)
             hw[p / 2] = (uint32_t)s_phi[p * NT + tid] | (uint32_t)s_phi[(p + 1) * NT + tid] << 16;
-        auto valid = [&](uint32_t p) { return p * NT + tid < n; };
+        // (k_ba_emit2 pads a partition's last runs with kBaPadHi pairs: not pairs of any key)
+        auto valid = [&](uint32_t p) {
+            return p * NT + tid < n && ((hw[p >> 1] >> (16 * (p & 1))) & 0xffffu) != kBaPadHi;
+        };
         const uint64_t w0 = (uint64_t)r * kBaRegionWords;
         const bool has_words = tid < NV && w0 + 4 * tid < nwords4;
         if (tid < NV) {
@@ -1012,6 +1165,10 @@ void set_add_rebucket_prefetch(int v) { g_rebucket_prefetch = v; }
 // into registers after this tile's hash (default), 0 = each tile loads its own
 static int g_stage1_prefetch = 1;
 void set_add_stage1_prefetch(int v) { g_stage1_prefetch = v; }
+// rbx_tune "add_rebucket_lines" (r05): 1 = the whole-line rebucket k_ba_emit2, 0 = k_ba_rebucket, 2 =
+// k_ba_emit2 when the chunk has >= 1024 stage-1 partitions (C2), else k_ba_rebucket (C1: 48)
+static int g_rebucket_lines = 0;
+void set_add_rebucket_lines(int v) { g_rebucket_lines = v; }
 
 template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
@@ -1036,11 +1193,19 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
 #define BA_REBUCKET(P6, ST, PF)                                                                                          \
     hipLaunchKernelGGL((k_ba_rebucket<P6, ST, PF>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, \
                        kBaSub, it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
-    if (g_region_kernel == 1) BA_REBUCKET(false, false, false);
+#define BA_EMIT2(ST)                                                                                                     \
+    hipLaunchKernelGGL((k_ba_emit2<6, ST>), dim3(nparts), dim3(1024), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub, a.s3, \
+                       a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
+    const uint32_t nparts = a.ncoarse * kBaSub;
+    const bool lines = g_region_kernel != 1 && (g_rebucket_lines == 1 || (g_rebucket_lines == 2 && nparts >= 1024));
+    if (lines && a.stamps) BA_EMIT2(true);
+    else if (lines) BA_EMIT2(false);
+    else if (g_region_kernel == 1) BA_REBUCKET(false, false, false);
     else if (a.stamps) BA_REBUCKET(true, true, true);
     else if (g_rebucket_prefetch) BA_REBUCKET(true, false, true);
     else BA_REBUCKET(true, false, false);
 #undef BA_REBUCKET
+#undef BA_EMIT2
     if (g_region_kernel == 1) {
         if (a.stamps)
             hipLaunchKernelGGL(k_ba_region<true>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,

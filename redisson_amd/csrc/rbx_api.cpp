@@ -3445,6 +3445,11 @@ int rbx_tune(const char *key, int value) {
         set_add_region_kernel(value);
         return RBX_OK;
     }
+    if (!strcmp(key, "add_rebucket_lines")) {
+        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rebucket_lines in {0, 1, 2}");
+        set_add_rebucket_lines(value);
+        return RBX_OK;
+    }
     if (!strcmp(key, "add_stage1_prefetch")) {
         if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_stage1_prefetch in {0, 1}");
         set_add_stage1_prefetch(value);

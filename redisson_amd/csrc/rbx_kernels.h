@@ -112,6 +112,7 @@ void set_add_region_kernel(int v);  // 1 (r02 8-byte pairs) or 2 (default: 6-byt
 void set_add_rec_lds_limit(int v);  // 0..7168 (tests)
 void set_add_rebucket_prefetch(int v);  // 0 or 1
 void set_add_stage1_prefetch(int v);  // 0 or 1
+void set_add_rebucket_lines(int v);   // 0 k_ba_rebucket, 1 k_ba_emit2 (whole-line runs), 2 by partition count
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 // Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB

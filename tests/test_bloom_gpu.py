@@ -1086,6 +1086,78 @@ def test_partitioned_add_overflow_falls_back(client, fresh):
     f.delete()
 
 
+ADD_REBUCKET_LINES_DEFAULT = 0
+
+
+@pytest.mark.parametrize("records", [1, 3, 0])
+def test_partitioned_add_whole_line_rebucket(client, fresh, records):
+    """r05 k_ba_emit2 (rbx_tune add_rebucket_lines 1, forced at every size): whole-line region runs,
+    remainders carried between tiles and a partition's last runs padded with pairs the region pass
+    skips.  Shapes of test_partitioned_add_parity (power-of-two and odd sizes, k 3..16, fixed and
+    variable-length keys), each with a batch that repeats keys within itself and re-adds earlier
+    ones; then the collision-table shape (every key twice in one region) and the overflow fallback.
+    Per-key flags, counts, bitmap bytes and count() vs the oracle."""
+    from redisson_amd import _lib as L_
+
+    assert L_.lib().rbx_tune(b"add_partition", 1) == 0
+    assert L_.lib().rbx_tune(b"add_records", records) == 0
+    assert L_.lib().rbx_tune(b"add_rebucket_lines", 1) == 0
+    try:
+        for j, (size, k, L) in enumerate([(1 << 32, 7, 32), (300_000_007, 10, 16), ((1 << 29) + 3, 16, 0),
+                                          (1 << 20, 3, 24)]):
+            rng = np.random.default_rng(9000 + 7 * j + records)
+            n = 200_000
+            if L:
+                mat = rng.integers(0, 256, size=(n, L), dtype=np.uint8)
+                second = np.concatenate([mat[n // 8: n // 2], mat[rng.integers(0, n // 2, size=n // 4)], mat[n // 2:]])
+                arenas = [(Arena.fixed(mat[: n // 4]), O.fixed_arena(mat[: n // 4])),
+                          (Arena.fixed(second), O.fixed_arena(second))]
+            else:
+                keys = [rng.bytes(int(x)) for x in rng.integers(0, 90, size=n)]
+                second = keys[n // 8: n // 2] + [keys[i] for i in rng.integers(0, n // 2, size=n // 4)] + keys[n // 2:]
+                arenas = [(Arena(keys[: n // 4]), O.arena(keys[: n // 4])), (Arena(second), O.arena(second))]
+            nm = f"{fresh}-{j}"
+            f = client.getBloomFilter(nm)
+            f.tryInitRaw(size, k)
+            ref = O.OracleBloom(size, k)
+            for a, o in arenas:
+                cg, ng = f.addEach(a)
+                cr, nr = ref.add(*o, per_key=True)
+                assert cg == cr and np.array_equal(ng, nr), (size, k, L)
+            assert f.exportBitmap() == ref.redis_string(), (size, k, L)
+            assert f.count() == ref.count()
+            f.delete()
+        # every key twice in one 2^16-bit region (collision-table rounds)
+        rng = np.random.default_rng(78 + records)
+        base = rng.integers(0, 256, size=(420, 24), dtype=np.uint8)
+        batch = np.concatenate([base, base[::-1], rng.integers(0, 256, size=(3, 24), dtype=np.uint8)])
+        f = client.getBloomFilter(f"{fresh}-c")
+        f.tryInitRaw(1 << 16, 7)
+        ref = O.OracleBloom(1 << 16, 7)
+        for b in (batch, batch[::3]):
+            cg, ng = f.addEach(Arena.fixed(b))
+            cr, nr = ref.add(*O.fixed_arena(b), per_key=True)
+            assert cg == cr and np.array_equal(ng, nr)
+        assert f.exportBitmap() == ref.redis_string()
+        f.delete()
+        # overflow: 40 keys repeated 400k times -> the chunk reruns on the first-setter table
+        base = rng.integers(0, 256, size=(40, 32), dtype=np.uint8)
+        batch = np.concatenate([base[rng.integers(0, 40, size=400_000)],
+                                rng.integers(0, 256, size=(30_000, 32), dtype=np.uint8)])
+        f = client.getBloomFilter(f"{fresh}-o")
+        f.tryInitRaw(1 << 30, 7)
+        ref = O.OracleBloom(1 << 30, 7)
+        cg, ng = f.addEach(Arena.fixed(batch))
+        cr, nr = ref.add(*O.fixed_arena(batch), per_key=True)
+        assert cg == cr and np.array_equal(ng, nr)
+        assert f.exportBitmap() == ref.redis_string()
+        f.delete()
+    finally:
+        L_.lib().rbx_tune(b"add_partition", 2)
+        L_.lib().rbx_tune(b"add_records", 2)
+        L_.lib().rbx_tune(b"add_rebucket_lines", ADD_REBUCKET_LINES_DEFAULT)
+
+
 def test_cross_stream_calls_run_in_call_order(client, fresh):
     """Device-path calls issued on different streams run in call order (the context's scratch and
     the bitmap are ordered by an event chain): add on stream A, then contains of the same keys on
@@ -1249,10 +1321,11 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
     keys[n - 1000:] = keys[:1000]  # repeats inside the batch
     dk = device_keys(keys.data_ptr(), n, 32)
-    runs = [(0, 2), (1, 0), (1, 1), (1, 3)]
+    # (add_partition, add_records, add_rebucket_lines): the whole-line rebucket with both report kinds
+    runs = [(0, 2, 0), (1, 0, 0), (1, 1, 0), (1, 3, 0), (1, 1, 1), (1, 3, 1)]
     flags, counts, bitmaps = [], [], []
     try:
-        for i, (part, rec) in enumerate(runs):
+        for i, (part, rec, lines) in enumerate(runs):
             nm = f"{fresh}-{i}"
             f = client.getBloomFilter(nm)
             f.tryInitRaw(1 << 32, 7)
@@ -1261,6 +1334,7 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
             out = torch.zeros((2, n), dtype=torch.uint8, device="cuda")
             L.lib().rbx_tune(b"add_partition", part)
             L.lib().rbx_tune(b"add_records", rec)
+            assert L.lib().rbx_tune(b"add_rebucket_lines", lines) == 0
             for j in range(2):  # second pass: every key already present
                 h.add_dev(dk, cnt.data_ptr() + 8 * j, out[j].data_ptr())
             torch.cuda.synchronize()
@@ -1272,6 +1346,7 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     finally:
         L.lib().rbx_tune(b"add_partition", 2)
         L.lib().rbx_tune(b"add_records", 2)
+        L.lib().rbx_tune(b"add_rebucket_lines", ADD_REBUCKET_LINES_DEFAULT)
     assert counts[0][1] == 0 and n - 1000 - 10 <= counts[0][0] <= n - 1000, counts[0]
     for i in range(1, len(runs)):
         assert counts[i] == counts[0], (runs[i], counts[i], counts[0])

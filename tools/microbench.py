@@ -267,6 +267,30 @@ def main():
         for dg, v in res.items():
             print(json.dumps({"bench": "add_partition_diag", "diag": dg, "ms_median": statistics.median(v)}), flush=True)
 
+    if "palines" in a.what:
+        # r05: the add's rebucket with whole-line runs (k_ba_emit2) vs k_ba_rebucket, n/2 keys into an
+        # empty 2^32-bit filter, interleaved, fresh filter per run; new-key counts must agree
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        m = n // 2
+        res, news = {0: [], 1: []}, {0: set(), 1: set()}
+        for rnd in range(4):
+            for ln in res:
+                assert L.lib().rbx_tune(b"add_rebucket_lines", ln) == 0
+                fb = client.getBloomFilter(f"pl-{rnd}-{ln}")
+                fb.tryInitRaw(1 << 32, 7)
+                h = BloomHandle(client, f"pl-{rnd}-{ln}")
+                cnt.zero_()
+                res[ln].append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(),
+                                                                stream=sp), 1))
+                news[ln].add(int(cnt[0].item()))
+                h.close()
+                fb.delete()
+        L.lib().rbx_tune(b"add_rebucket_lines", 0)
+        assert news[0] == news[1] and len(news[0]) == 1, news
+        for ln, v in res.items():
+            print(json.dumps({"bench": "add_rebucket_lines", "lines": ln, "ms": v, "ms_median": statistics.median(v),
+                              "new": min(news[ln])}), flush=True)
+
     if "regstamp" in a.what:
         # region-pass phase times (add_partition_diag 64, exact results) of each region kernel,
         # C2 add of n/2 keys into an empty 2^32-bit filter; summed over blocks, in ms of one CU's
