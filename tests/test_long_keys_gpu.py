@@ -153,3 +153,29 @@ def test_long_keys_ordered_stream(client, fresh):
         h.close()
     for nm in names:
         client.getBloomFilter(nm).delete()
+
+
+def test_long_elements_hll(client, fresh):
+    """PFADD of long elements (MurmurHash64A over many 8-byte blocks and every tail length, [redis-7.2]
+    hllPatLen): a sparse HLL (the string as Redis builds it, element by element) and a dense one
+    (registers and PFCOUNT)."""
+    rng = np.random.default_rng(0x411)
+    lens = [0, 1, 7, 8, 9, 15, 16, 17, 63, 64, 65, 1000, 4095, 4096, 4097, 9999]
+    few = [rng.bytes(x) for x in lens] + [rng.bytes(int(x)) for x in rng.integers(0, 3000, size=150)]
+    ref = O.RedisHll()
+    ref.pfadd(*O.arena(few))
+    h = client.getHyperLogLog(fresh)
+    assert h.addAll(Arena(few)) is True
+    s = h.exportString()
+    assert s[4] == 1 and s == ref.string(h.exportDense()[8:16])
+    assert h.count() == O.hll_count(ref.regs)
+    many = few + [rng.bytes(int(x)) for x in rng.integers(0, 2500, size=20000)]
+    g = client.getHyperLogLog(fresh + "d")
+    assert g.addAll(Arena(many)) is True
+    regs = O.hll_new()
+    O.hll_pfadd(regs, *O.arena(many))
+    d = g.exportDense()
+    assert np.array_equal(O.hll_dense_unpack(d[16:]), regs)
+    assert g.count() == O.hll_count(regs)
+    h.delete()
+    g.delete()
