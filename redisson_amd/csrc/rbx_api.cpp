@@ -236,6 +236,9 @@ struct rbx_ctx {
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf slot_bytes[2], slot_offs[2];
     uint64_t staging_bytes = 64ull << 20;
+    // small host batches (bloom_host_small): a pinned copy of the keys, uploaded on `stream` with the
+    // zeroed count word in one transfer; the count and flags come back into it
+    void *pin_small = nullptr;
 
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
     hipEvent_t ev_scratch = nullptr;
@@ -907,6 +910,8 @@ int rbx_shutdown(rbx_ctx *c) {
         }
         if (c->ev_scratch) (void)hipEventDestroy(c->ev_scratch);
         c->ev_scratch = nullptr;
+        if (c->pin_small) (void)hipHostFree(c->pin_small);
+        c->pin_small = nullptr;
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->copy_stream = c->stream = nullptr;
@@ -1105,6 +1110,59 @@ static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t 
     return RBX_OK;
 }
 
+// Small host batches -- the single-key add(T) / contains(T) Redisson sends most, and collections of up
+// to kSmallKeys keys / kSmallBytes of key bytes: the keys are copied into pinned memory behind a zero
+// count word and uploaded on the context stream in ONE transfer (no copy-stream hand-off, no sync before
+// the launch: the slot's previous reader is waited for by its event), and the count and flags come back
+// into the same pinned block with one sync.  (The pipelined path costs a fill, a sync, a copy-stream
+// upload from pageable memory with two event hops, and a second sync: ~62 us for one key on the r05
+// boxes, tools/microbench.py smallbatch.)
+static constexpr uint64_t kSmallKeys = 65536, kSmallBytes = 256 << 10;
+static int g_small_host = 1;  // rbx_tune("host_small_batches"): 0 = every host batch on the pipelined path
+static constexpr size_t kSmallPin = 64 + kSmallBytes + kSmallKeys + 64;  // count | keys (+ offsets) | flags
+
+static bool bloom_small_fits(const rbx_keys *k) {
+    if (k->n == 0 || k->n > kSmallKeys) return false;
+    const uint64_t nb = k->offsets ? k->offsets[k->n] - k->offsets[0] : k->n * k->stride;
+    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= kSmallBytes;
+}
+
+static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
+                            uint64_t *out_count, bool is_add) {
+    if (!c->pin_small) HIP_TRY(hipHostMalloc(&c->pin_small, kSmallPin, hipHostMallocDefault));
+    uint8_t *hp = (uint8_t *)c->pin_small;
+    const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
+    const uint64_t nb = keys->offsets ? keys->offsets[n] - b0 : n * keys->stride;
+    const uint64_t off_at = keys->offsets ? (64 + nb + 7) / 8 * 8 : 0, end = off_at ? off_at + (n + 1) * 8 : 64 + nb;
+    memset(hp, 0, 8);
+    if (nb) memcpy(hp + 64, keys->bytes + b0, nb);
+    if (off_at) memcpy(hp + off_at, keys->offsets, (n + 1) * 8);  // absolute offsets: KeysDev.off_base = b0
+    RBX_TRY(c->slot_bytes[0].reserve(kSmallPin));
+    uint8_t *dp = c->slot_bytes[0].as<uint8_t>();
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_done[0], 0));  // slot 0's last reader (any stream)
+    HIP_TRY(hipMemcpyAsync(dp, hp, end, hipMemcpyHostToDevice, c->stream));
+    uint8_t *d_out = nullptr;
+    if (out_flags) {
+        RBX_TRY(c->out_bytes.reserve(n));
+        d_out = c->out_bytes.as<uint8_t>();
+    }
+    KeysDev dk{dp + 64, off_at ? (const uint64_t *)(dp + off_at) : nullptr, keys->stride, n, off_at ? b0 : 0};
+    auto *d_count = (unsigned long long *)dp;
+    const int rc = is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream)
+                          : run_contains(c, dk, f, d_out, d_count, c->stream);
+    (void)hipEventRecord(c->ev_done[0], c->stream);  // slot 0 read by what was queued, whatever rc
+    RBX_TRY(rc);
+    // the readback lands in the pinned block: its upload precedes it on the stream
+    HIP_TRY(hipMemcpyAsync(hp, dp, 8, hipMemcpyDeviceToHost, c->stream));
+    if (out_flags) HIP_TRY(hipMemcpyAsync(hp + 64 + kSmallBytes, d_out, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out_flags) memcpy(out_flags, hp + 64 + kSmallBytes, n);
+    uint64_t cnt;
+    memcpy(&cnt, hp, 8);
+    if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
+    return RBX_OK;
+}
+
 static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint32_t k, const rbx_keys *keys,
                          uint8_t *out_flags, uint64_t *out_count, bool is_add) {
     RBX_TRY(validate_keys(keys));
@@ -1138,6 +1196,8 @@ static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint
         if (out_count) *out_count = 0;
         return RBX_OK;
     }
+    FilterDesc f = desc_of(*bm, size_bits(size), k, 0);
+    if (g_small_host && bloom_small_fits(keys)) return bloom_host_small(c, f, k, keys, out_flags, out_count, is_add);
     RBX_TRY(c->counters.reserve(64));
     auto *d_count = c->counters.as<unsigned long long>();
     HIP_TRY(hipMemsetAsync(d_count, 0, 8, c->stream));
@@ -1146,7 +1206,6 @@ static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint
         RBX_TRY(c->out_bytes.reserve(keys->n));
         d_out = c->out_bytes.as<uint8_t>();
     }
-    FilterDesc f = desc_of(*bm, size_bits(size), k, 0);
     HIP_TRY(hipStreamSynchronize(c->stream));  // slots may still be read by an earlier call's stream
     RBX_TRY(pipelined_host_batches(c, keys, c->stream, [&](const KeysDev &dk, uint64_t i0) -> int {
         uint8_t *o = d_out ? d_out + i0 : nullptr;
@@ -3443,6 +3502,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_region_kernel")) {
         if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_kernel in {1, 2}");
         set_add_region_kernel(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "host_small_batches")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "host_small_batches in {0, 1}");
+        g_small_host = value;
         return RBX_OK;
     }
     if (!strcmp(key, "add_rebucket_lines")) {

@@ -929,6 +929,45 @@ def test_host_path_pipelined_chunks(client, fresh, staging):
     f.delete()
 
 
+@pytest.mark.parametrize("small", [1, 0])
+def test_host_small_batches(client, fresh, small):
+    """r05: host batches of <= 65,536 keys and 256 KiB take the one-transfer path (bloom_host_small:
+    pinned copy, one upload with the zeroed count, one readback); with it on (1) and off (0): single
+    keys, batches of 256 KiB and 256 KiB + 16 bytes, variable-length keys under and over the
+    limit, empty keys, and a large pipelined batch in between -- add and contains, per-key flags and
+    counts, then the bitmap, vs the oracle."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(0x5A11 + small)
+    f = client.getBloomFilter(fresh)
+    f.tryInit(100_000, 0.01)
+    ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+    mats = [rng.integers(0, 256, size=(n, 16), dtype=np.uint8) for n in (1, 1, 4096, 16384, 16385, 200_000)]
+    var = [[rng.bytes(int(x)) for x in rng.integers(0, 91, size=500)],
+           [rng.bytes(int(x)) for x in rng.integers(66, 76, size=4000)],  # ~280 KB: past the limit
+           [b""] * 100]
+    batches = [(Arena.fixed(m), O.fixed_arena(m)) for m in mats[:2]] + [(Arena(v), O.arena(v)) for v in var] + \
+              [(Arena.fixed(m), O.fixed_arena(m)) for m in mats[2:]] + [(Arena.fixed(mats[0]), O.fixed_arena(mats[0]))]
+    assert L_.lib().rbx_tune(b"host_small_batches", small) == 0
+    try:
+        for a, o in batches:
+            cg, ng = f.addEach(a)
+            cr, nr = ref.add(*o, per_key=True)
+            assert cg == cr and np.array_equal(ng, nr)
+            assert f.add(a) == ref.add(*o)  # again: every key present, count only
+            cg, pg = f.containsEach(a)
+            cr, pr = ref.contains(*o, per_key=True)
+            assert cg == cr and np.array_equal(pg, pr)
+        one = [bytes(mats[4][7]), b"never-added-key"]
+        for key in one:  # contains(T) / add(T) shapes: one key per call
+            assert f.contains(Arena([key])) == ref.contains(*O.arena([key]))
+    finally:
+        L_.lib().rbx_tune(b"host_small_batches", 1)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.count() == ref.count()
+    f.delete()
+
+
 def test_pinned_host_arena(client, fresh):
     """Keys in rbx_host_alloc (pinned) memory go through the same path."""
     import ctypes as C

@@ -267,6 +267,61 @@ def main():
         for dg, v in res.items():
             print(json.dumps({"bench": "add_partition_diag", "diag": dg, "ms_median": statistics.median(v)}), flush=True)
 
+    if "smallbatch" in a.what:
+        # per-call latency of the batch sizes Redisson callers send (contains(T) / add(T) are one key) on the
+        # C1 filter (tryInit(1e7, 0.01), 1M keys added): the synchronous by-name host-arena calls
+        # (rbx_bloom_contains / rbx_bloom_add: name lookup, staging upload, kernel, result readback) and
+        # the handle calls on keys already in HBM plus a stream sync; median wall time of 300 calls
+        import time
+
+        import numpy as np
+
+        from redisson_amd import Arena
+
+        fb = client.getBloomFilter("sb")
+        fb.tryInit(10_000_000, 0.01)
+        h = BloomHandle(client, "sb")
+        base = torch.randint(0, 256, (1_000_000, 16), dtype=torch.uint8, device="cuda", generator=g)
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        h.add_dev(device_keys(base.data_ptr(), 1_000_000, 16), cnt.data_ptr(), stream=sp)
+        torch.cuda.synchronize()
+        rng = np.random.default_rng(5)
+        hostkeys = base[:65536].cpu().numpy()
+        fresh = torch.randint(0, 256, (300 * 4096, 16), dtype=torch.uint8, device="cuda", generator=g)
+        for nb in [1, 16, 256, 4096, 65536]:
+            res = {}
+            present = Arena.fixed(hostkeys[:nb])
+            adds = [Arena.fixed(rng.integers(0, 256, size=(nb, 16), dtype=np.uint8)) for _ in range(20)]
+            calls = {
+                "contains_host": lambda i: fb.contains(present),
+                "add_host": lambda i: fb.add(adds[i % 20]),
+                "contains_dev": lambda i: (h.contains_dev(device_keys(base.data_ptr(), nb, 16), cnt.data_ptr() + 8,
+                                                          stream=sp), stream.synchronize()),
+                "add_dev": lambda i: (h.add_dev(device_keys(fresh.data_ptr() + 16 * ((i * nb) % (fresh.shape[0] - nb)),
+                                                            nb, 16), cnt.data_ptr(), stream=sp), stream.synchronize()),
+            }
+            if nb == 1:
+                calls["contains_one_object"] = lambda i: fb.contains(bytes(hostkeys[0]))
+            if nb <= 256:  # PFADD of nb host elements: a dense HLL, and a sparse one (a new HLL every 20 calls)
+                hd = client.getHyperLogLog(f"sb-hd-{nb}")
+                hd.addAll(Arena.fixed(rng.integers(0, 256, size=(200_000, 16), dtype=np.uint8)))
+                calls["pfadd_dense_host"] = lambda i: hd.addAll(adds[i % 20])
+                calls["pfadd_sparse_host"] = lambda i: client.getHyperLogLog(f"sb-hs-{nb}-{i // 20}").addAll(
+                    adds[i % 20])
+                calls["pfcount_dense_host"] = lambda i: hd.count()
+            for kind, fn in calls.items():
+                for i in range(20):
+                    fn(i)
+                ts = []
+                for i in range(300):
+                    t0 = time.perf_counter()
+                    fn(i)
+                    ts.append(time.perf_counter() - t0)
+                res[kind] = round(statistics.median(ts) * 1e6, 1)
+            print(json.dumps({"bench": "smallbatch", "keys": nb, "median_us": res}), flush=True)
+        h.close()
+        fb.delete()
+
     if "palines" in a.what:
         # r05: the add's rebucket with whole-line runs (k_ba_emit2) vs k_ba_rebucket, n/2 keys into an
         # empty 2^32-bit filter, interleaved, fresh filter per run; new-key counts must agree
