@@ -57,9 +57,11 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           region-pass phase times, read by rbx_bench_add_stamps)
  *   "add_region_kernel"     partitioned add region pass: 2 (default: 6-byte region pairs,
  *                           pipelined k_ba_region6), 1 (8-byte pairs, k_ba_region)
- *   "host_small_batches"    1 (default): host-arena add/contains batches of <= 65,536 keys and
- *                           256 KiB take the one-transfer path (pinned copy, one upload, one
- *                           readback); 0: every host batch on the pipelined copy-stream path
+ *   "host_small_batches"    1 (default): host-arena add/contains batches within host_small_bytes
+ *                           take the one-transfer path (pinned copy, one upload, one readback);
+ *                           0: every host batch on the pipelined copy-stream path
+ *   "host_small_bytes"      that path's limit: key bytes (+ offsets), 4 KiB .. 64 MiB (default
+ *                           4 MiB; at most a quarter as many keys)
  *   "add_rebucket_lines"    partitioned add rebucket: 0 (default) k_ba_rebucket, 1 k_ba_emit2
  *                           (whole-line region runs, LDS carries; measured 0.03 ms slower at C2),
  *                           2 k_ba_emit2 when a chunk has >= 1024 stage-1 partitions

@@ -239,6 +239,7 @@ struct rbx_ctx {
     // small host batches (bloom_host_small): a pinned copy of the keys, uploaded on `stream` with the
     // zeroed count word in one transfer; the count and flags come back into it
     void *pin_small = nullptr;
+    size_t pin_small_cap = 0;
 
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
     hipEvent_t ev_scratch = nullptr;
@@ -475,11 +476,10 @@ static int upload_keys(rbx_ctx *c, const rbx_keys *k, uint64_t i0, uint64_t i1, 
         RBX_TRY(c->keys_bytes.reserve(b1 - b0 + 16));
         RBX_TRY(c->keys_offs.reserve((n + 1) * 8));
         if (b1 > b0) HIP_TRY(hipMemcpyAsync(c->keys_bytes.p, k->bytes + b0, b1 - b0, hipMemcpyHostToDevice, c->stream));
-        std::vector<uint64_t> offs(n + 1);
-        for (uint64_t i = 0; i <= n; ++i) offs[i] = k->offsets[i0 + i] - b0;
-        HIP_TRY(hipMemcpyAsync(c->keys_offs.p, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));  // `offs` is a stack vector
-        *out = KeysDev{c->keys_bytes.as<uint8_t>(), c->keys_offs.as<uint64_t>(), 0, n};
+        // the caller's offsets as they are (the kernels subtract off_base): no rebased copy on the stack,
+        // so no sync before returning (a pageable source is staged by the runtime before the call returns)
+        HIP_TRY(hipMemcpyAsync(c->keys_offs.p, k->offsets + i0, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        *out = KeysDev{c->keys_bytes.as<uint8_t>(), c->keys_offs.as<uint64_t>(), 0, n, b0};
     } else {
         uint64_t bytes = n * k->stride;
         RBX_TRY(c->keys_bytes.reserve(bytes + 16));
@@ -912,6 +912,7 @@ int rbx_shutdown(rbx_ctx *c) {
         c->ev_scratch = nullptr;
         if (c->pin_small) (void)hipHostFree(c->pin_small);
         c->pin_small = nullptr;
+        c->pin_small_cap = 0;
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->copy_stream = c->stream = nullptr;
@@ -1111,25 +1112,32 @@ static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t 
 }
 
 // Small host batches -- the single-key add(T) / contains(T) Redisson sends most, and collections of up
-// to kSmallKeys keys / kSmallBytes of key bytes: the keys are copied into pinned memory behind a zero
+// to host_small_bytes of key bytes (and a quarter as many keys): the keys are copied into pinned memory behind a zero
 // count word and uploaded on the context stream in ONE transfer (no copy-stream hand-off, no sync before
 // the launch: the slot's previous reader is waited for by its event), and the count and flags come back
 // into the same pinned block with one sync.  (The pipelined path costs a fill, a sync, a copy-stream
 // upload from pageable memory with two event hops, and a second sync: ~62 us for one key on the r05
 // boxes, tools/microbench.py smallbatch.)
-static constexpr uint64_t kSmallKeys = 65536, kSmallBytes = 256 << 10;
 static int g_small_host = 1;  // rbx_tune("host_small_batches"): 0 = every host batch on the pipelined path
-static constexpr size_t kSmallPin = 64 + kSmallBytes + kSmallKeys + 64;  // count | keys (+ offsets) | flags
+static uint64_t g_small_bytes = 4 << 20;  // rbx_tune("host_small_bytes"): the byte limit (keys <= limit / 4)
+static size_t small_pin_bytes() { return 64 + g_small_bytes + g_small_bytes / 4 + 64; }  // count | keys | flags
 
 static bool bloom_small_fits(const rbx_keys *k) {
-    if (k->n == 0 || k->n > kSmallKeys) return false;
+    if (k->n == 0 || k->n > g_small_bytes / 4) return false;
     const uint64_t nb = k->offsets ? k->offsets[k->n] - k->offsets[0] : k->n * k->stride;
-    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= kSmallBytes;
+    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= g_small_bytes;
 }
 
 static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
                             uint64_t *out_count, bool is_add) {
-    if (!c->pin_small) HIP_TRY(hipHostMalloc(&c->pin_small, kSmallPin, hipHostMallocDefault));
+    const size_t pin = small_pin_bytes();
+    if (c->pin_small_cap < pin) {
+        if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
+        c->pin_small = nullptr;
+        c->pin_small_cap = 0;
+        HIP_TRY(hipHostMalloc(&c->pin_small, pin, hipHostMallocDefault));
+        c->pin_small_cap = pin;
+    }
     uint8_t *hp = (uint8_t *)c->pin_small;
     const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
     const uint64_t nb = keys->offsets ? keys->offsets[n] - b0 : n * keys->stride;
@@ -1137,7 +1145,7 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
     memset(hp, 0, 8);
     if (nb) memcpy(hp + 64, keys->bytes + b0, nb);
     if (off_at) memcpy(hp + off_at, keys->offsets, (n + 1) * 8);  // absolute offsets: KeysDev.off_base = b0
-    RBX_TRY(c->slot_bytes[0].reserve(kSmallPin));
+    RBX_TRY(c->slot_bytes[0].reserve(pin));
     uint8_t *dp = c->slot_bytes[0].as<uint8_t>();
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_done[0], 0));  // slot 0's last reader (any stream)
     HIP_TRY(hipMemcpyAsync(dp, hp, end, hipMemcpyHostToDevice, c->stream));
@@ -1154,9 +1162,9 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
     RBX_TRY(rc);
     // the readback lands in the pinned block: its upload precedes it on the stream
     HIP_TRY(hipMemcpyAsync(hp, dp, 8, hipMemcpyDeviceToHost, c->stream));
-    if (out_flags) HIP_TRY(hipMemcpyAsync(hp + 64 + kSmallBytes, d_out, n, hipMemcpyDeviceToHost, c->stream));
+    if (out_flags) HIP_TRY(hipMemcpyAsync(hp + 64 + g_small_bytes, d_out, n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (out_flags) memcpy(out_flags, hp + 64 + kSmallBytes, n);
+    if (out_flags) memcpy(out_flags, hp + 64 + g_small_bytes, n);
     uint64_t cnt;
     memcpy(&cnt, hp, 8);
     if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
@@ -3502,6 +3510,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_region_kernel")) {
         if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_kernel in {1, 2}");
         set_add_region_kernel(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "host_small_bytes")) {
+        if (value < 4096 || value > (64 << 20)) return fail(RBX_E_ILLEGAL_ARGUMENT, "host_small_bytes in [4 KiB, 64 MiB]");
+        g_small_bytes = (uint64_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "host_small_batches")) {

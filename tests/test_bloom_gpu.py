@@ -931,7 +931,7 @@ def test_host_path_pipelined_chunks(client, fresh, staging):
 
 @pytest.mark.parametrize("small", [1, 0])
 def test_host_small_batches(client, fresh, small):
-    """r05: host batches of <= 65,536 keys and 256 KiB take the one-transfer path (bloom_host_small:
+    """r05: host batches within host_small_bytes (here 256 KiB; default 4 MiB) take the one-transfer path (bloom_host_small:
     pinned copy, one upload with the zeroed count, one readback); with it on (1) and off (0): single
     keys, batches of 256 KiB and 256 KiB + 16 bytes, variable-length keys under and over the
     limit, empty keys, and a large pipelined batch in between -- add and contains, per-key flags and
@@ -949,6 +949,7 @@ def test_host_small_batches(client, fresh, small):
     batches = [(Arena.fixed(m), O.fixed_arena(m)) for m in mats[:2]] + [(Arena(v), O.arena(v)) for v in var] + \
               [(Arena.fixed(m), O.fixed_arena(m)) for m in mats[2:]] + [(Arena.fixed(mats[0]), O.fixed_arena(mats[0]))]
     assert L_.lib().rbx_tune(b"host_small_batches", small) == 0
+    assert L_.lib().rbx_tune(b"host_small_bytes", 256 << 10) == 0  # the batches straddle this limit
     try:
         for a, o in batches:
             cg, ng = f.addEach(a)
@@ -963,6 +964,7 @@ def test_host_small_batches(client, fresh, small):
             assert f.contains(Arena([key])) == ref.contains(*O.arena([key]))
     finally:
         L_.lib().rbx_tune(b"host_small_batches", 1)
+        L_.lib().rbx_tune(b"host_small_bytes", 4 << 20)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()
