@@ -1120,7 +1120,8 @@ static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t 
 // boxes, tools/microbench.py smallbatch.)
 static int g_small_host = 1;  // rbx_tune("host_small_batches"): 0 = every host batch on the pipelined path
 static uint64_t g_small_bytes = 4 << 20;  // rbx_tune("host_small_bytes"): the byte limit (keys <= limit / 4)
-static size_t small_pin_bytes() { return 64 + g_small_bytes + g_small_bytes / 4 + 64; }  // count | keys | flags
+static constexpr uint64_t kSmallHead = 64 << 10;  // zeroed result area ahead of the keys (counts, changed words)
+static size_t small_pin_bytes() { return kSmallHead + g_small_bytes + g_small_bytes / 4 + 64; }  // head | keys | tail
 
 static bool bloom_small_fits(const rbx_keys *k) {
     if (k->n == 0 || k->n > g_small_bytes / 4) return false;
@@ -1128,8 +1129,15 @@ static bool bloom_small_fits(const rbx_keys *k) {
     return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= g_small_bytes;
 }
 
-static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
-                            uint64_t *out_count, bool is_add) {
+// One-transfer staging of a small host arena (bloom_small_fits): pinned [0, head) zeroed, the key bytes
+// from `head`, then the offsets (absolute: KeysDev.off_base), uploaded with one copy into staging slot 0
+// on the context stream after slot 0's last reader (its event).  The caller records c->ev_done[0] after
+// its launches, reads results back into hp / tail_h and syncs; the pinned block stays untouched until then.
+struct SmallStage {
+    uint8_t *hp = nullptr, *dp = nullptr, *tail_h = nullptr;  // pinned block, its device copy, readback area
+    KeysDev dk{};
+};
+static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallStage *s) {
     const size_t pin = small_pin_bytes();
     if (c->pin_small_cap < pin) {
         if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
@@ -1138,35 +1146,47 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
         HIP_TRY(hipHostMalloc(&c->pin_small, pin, hipHostMallocDefault));
         c->pin_small_cap = pin;
     }
+    head = (std::max<uint64_t>(head, 8) + 63) / 64 * 64;  // <= kSmallHead (callers bound it)
     uint8_t *hp = (uint8_t *)c->pin_small;
     const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
     const uint64_t nb = keys->offsets ? keys->offsets[n] - b0 : n * keys->stride;
-    const uint64_t off_at = keys->offsets ? (64 + nb + 7) / 8 * 8 : 0, end = off_at ? off_at + (n + 1) * 8 : 64 + nb;
-    memset(hp, 0, 8);
-    if (nb) memcpy(hp + 64, keys->bytes + b0, nb);
-    if (off_at) memcpy(hp + off_at, keys->offsets, (n + 1) * 8);  // absolute offsets: KeysDev.off_base = b0
+    const uint64_t off_at = keys->offsets ? (head + nb + 7) / 8 * 8 : 0, end = off_at ? off_at + (n + 1) * 8 : head + nb;
+    memset(hp, 0, head);
+    if (nb) memcpy(hp + head, keys->bytes + b0, nb);
+    if (off_at) memcpy(hp + off_at, keys->offsets, (n + 1) * 8);
     RBX_TRY(c->slot_bytes[0].reserve(pin));
     uint8_t *dp = c->slot_bytes[0].as<uint8_t>();
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_done[0], 0));  // slot 0's last reader (any stream)
     HIP_TRY(hipMemcpyAsync(dp, hp, end, hipMemcpyHostToDevice, c->stream));
+    s->hp = hp;
+    s->dp = dp;
+    s->tail_h = hp + kSmallHead + g_small_bytes;
+    s->dk = KeysDev{dp + head, off_at ? (const uint64_t *)(dp + off_at) : nullptr, keys->stride, n, off_at ? b0 : 0};
+    return RBX_OK;
+}
+
+static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
+                            uint64_t *out_count, bool is_add) {
+    SmallStage s;
+    RBX_TRY(small_stage(c, keys, 8, &s));
+    const uint64_t n = keys->n;
     uint8_t *d_out = nullptr;
     if (out_flags) {
         RBX_TRY(c->out_bytes.reserve(n));
         d_out = c->out_bytes.as<uint8_t>();
     }
-    KeysDev dk{dp + 64, off_at ? (const uint64_t *)(dp + off_at) : nullptr, keys->stride, n, off_at ? b0 : 0};
-    auto *d_count = (unsigned long long *)dp;
-    const int rc = is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream)
-                          : run_contains(c, dk, f, d_out, d_count, c->stream);
+    auto *d_count = (unsigned long long *)s.dp;
+    const int rc = is_add ? run_add(c, s.dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream)
+                          : run_contains(c, s.dk, f, d_out, d_count, c->stream);
     (void)hipEventRecord(c->ev_done[0], c->stream);  // slot 0 read by what was queued, whatever rc
     RBX_TRY(rc);
     // the readback lands in the pinned block: its upload precedes it on the stream
-    HIP_TRY(hipMemcpyAsync(hp, dp, 8, hipMemcpyDeviceToHost, c->stream));
-    if (out_flags) HIP_TRY(hipMemcpyAsync(hp + 64 + g_small_bytes, d_out, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(s.hp, s.dp, 8, hipMemcpyDeviceToHost, c->stream));
+    if (out_flags) HIP_TRY(hipMemcpyAsync(s.tail_h, d_out, n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (out_flags) memcpy(out_flags, hp + 64 + g_small_bytes, n);
+    if (out_flags) memcpy(out_flags, s.tail_h, n);
     uint64_t cnt;
-    memcpy(&cnt, hp, 8);
+    memcpy(&cnt, s.hp, 8);
     if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
     return RBX_OK;
 }
@@ -2179,6 +2199,23 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         hl[s] = keep[s].get();
         created[s] = cr;
     }
+    std::vector<uint32_t> ch(nseg);
+    if (g_small_host && nseg <= kSmallHead / 4 && bloom_small_fits(elements)) {
+        // one transfer for the elements and the zeroed changed words, one readback (bloom_host_small)
+        SmallStage sm;
+        RBX_TRY(small_stage(c, elements, nseg * 4, &sm));
+        const int rc = pfadd_run(c, hl, seg_offsets, sm.dk, (uint32_t *)sm.dp, c->stream);
+        (void)hipEventRecord(c->ev_done[0], c->stream);
+        RBX_TRY(rc);
+        HIP_TRY(hipMemcpyAsync(sm.hp, sm.dp, nseg * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        memcpy(ch.data(), sm.hp, nseg * 4);
+        for (uint32_t s = 0; s < nseg; ++s) {
+            if (ch[s]) hl[s]->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+            if (out_changed) out_changed[s] = ch[s] || created[s];
+        }
+        return RBX_OK;
+    }
     RBX_TRY(c->misc.reserve(nseg * 4));
     auto *d_changed = c->misc.as<uint32_t>();
     HIP_TRY(hipMemsetAsync(d_changed, 0, nseg * 4, c->stream));
@@ -2199,7 +2236,6 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         RBX_TRY(pfadd_run(c, grp, reb.data(), dk, d_changed + s0, c->stream));
         s0 = s1;
     }
-    std::vector<uint32_t> ch(nseg);
     HIP_TRY(hipMemcpyAsync(ch.data(), d_changed, nseg * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (uint32_t s = 0; s < nseg; ++s) {
