@@ -467,8 +467,8 @@ static int validate_keys(const rbx_keys *k) {
     return RBX_OK;
 }
 
-// Copies keys [i0, i1) of a host arena to device buffers; returns device view with
-// keys renumbered from 0.
+// Copies keys [i0, i1) of a host arena to device buffers; returns a device view with keys renumbered
+// from 0 (the offsets as the caller's: KeysDev.off_base = offsets[i0]).
 static int upload_keys(rbx_ctx *c, const rbx_keys *k, uint64_t i0, uint64_t i1, KeysDev *out) {
     uint64_t n = i1 - i0;
     if (k->offsets) {
@@ -1979,7 +1979,8 @@ int rbx_bloom_stream(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, c
         RBX_TRY(c->out_bytes.reserve(n));
         d_out = c->out_bytes.as<uint8_t>();
     }
-    rbx_keys kd{dk.bytes, dk.offsets, dk.stride, dk.n};
+    // the *_dev ABI has no off_base: shift the base so that bytes + offsets[i] is key i (never read below)
+    rbx_keys kd{dk.bytes - dk.off_base, dk.offsets, dk.stride, dk.n};
     RBX_TRY(rbx_bloom_stream_dev(c, filters, nfilters, d_kf, d_op, &kd, d_out, d_cnt, c->stream));
     if (out && n) HIP_TRY(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, c->stream));
     unsigned long long cnt[2];
@@ -2017,7 +2018,8 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
         RBX_TRY(c->out_bytes.reserve(keys->n));
         d_out = c->out_bytes.as<uint8_t>();
     }
-    rbx_keys kd{dk.bytes, dk.offsets, dk.stride, dk.n};
+    // the *_dev ABI has no off_base: shift the base so that bytes + offsets[i] is key i (never read below)
+    rbx_keys kd{dk.bytes - dk.off_base, dk.offsets, dk.stride, dk.n};
     if (is_add) {
         uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
         for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
