@@ -1137,7 +1137,8 @@ struct SmallStage {
     uint8_t *hp = nullptr, *dp = nullptr, *tail_h = nullptr;  // pinned block, its device copy, readback area
     KeysDev dk{};
 };
-static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallStage *s) {
+static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallStage *s, const void *head_src = nullptr,
+                       uint64_t head_src_at = 0, uint64_t head_src_len = 0) {
     const size_t pin = small_pin_bytes();
     if (c->pin_small_cap < pin) {
         if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
@@ -1152,6 +1153,7 @@ static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallSta
     const uint64_t nb = keys->offsets ? keys->offsets[n] - b0 : n * keys->stride;
     const uint64_t off_at = keys->offsets ? (head + nb + 7) / 8 * 8 : 0, end = off_at ? off_at + (n + 1) * 8 : head + nb;
     memset(hp, 0, head);
+    if (head_src_len) memcpy(hp + head_src_at, head_src, head_src_len);  // e.g. segment offsets behind the counts
     if (nb) memcpy(hp + head, keys->bytes + b0, nb);
     if (off_at) memcpy(hp + off_at, keys->offsets, (n + 1) * 8);
     RBX_TRY(c->slot_bytes[0].reserve(pin));
@@ -2006,6 +2008,39 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
     std::lock_guard<std::recursive_mutex> g(c->ks.mu);
     RBX_TRY(set_device(c));
     ScratchOrder so_(c, c->stream);
+    uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
+    for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
+    if (g_small_host && (uint64_t)nseg * 16 + 8 <= kSmallHead && bloom_small_fits(keys)) {
+        // one transfer: the zeroed per-segment counts, the segment offsets, the keys (bloom_host_small)
+        SmallStage sm;
+        const uint64_t so_at = (uint64_t)nseg * 8;
+        RBX_TRY(small_stage(c, keys, so_at + (uint64_t)(nseg + 1) * 8, &sm, seg_offsets, so_at, (uint64_t)(nseg + 1) * 8));
+        auto *d_counts = (unsigned long long *)sm.dp;
+        const auto *d_seg = (const uint64_t *)(sm.dp + so_at);
+        uint8_t *d_out = nullptr;
+        if (out_flags) {
+            RBX_TRY(c->out_bytes.reserve(keys->n));
+            d_out = c->out_bytes.as<uint8_t>();
+        }
+        // the *_dev ABI has no off_base: shift the base so that bytes + offsets[i] is key i
+        rbx_keys kd{sm.dk.bytes - sm.dk.off_base, sm.dk.offsets, sm.dk.stride, sm.dk.n};
+        int rc;
+        if (is_add) {
+            c->madd_maxseg_hint = mx;
+            rc = rbx_bloom_add_multi_dev(c, filters, nseg, d_seg, &kd, d_out, d_counts, c->stream);
+            c->madd_maxseg_hint = ~0ULL;
+        } else {
+            rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_out, d_counts, c->stream);
+        }
+        (void)hipEventRecord(c->ev_done[0], c->stream);
+        RBX_TRY(rc);
+        HIP_TRY(hipMemcpyAsync(sm.hp, sm.dp, (size_t)nseg * 8, hipMemcpyDeviceToHost, c->stream));
+        if (out_flags) HIP_TRY(hipMemcpyAsync(sm.tail_h, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (out_flags) memcpy(out_flags, sm.tail_h, keys->n);
+        if (out_counts) memcpy(out_counts, sm.hp, (size_t)nseg * 8);
+        return RBX_OK;
+    }
     KeysDev dk;
     RBX_TRY(upload_keys(c, keys, 0, keys->n, &dk));
     RBX_TRY(c->seg_offs.reserve((nseg + 1) * 8));
@@ -2021,8 +2056,6 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
     // the *_dev ABI has no off_base: shift the base so that bytes + offsets[i] is key i (never read below)
     rbx_keys kd{dk.bytes - dk.off_base, dk.offsets, dk.stride, dk.n};
     if (is_add) {
-        uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
-        for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
         c->madd_maxseg_hint = mx;
         const int rc = rbx_bloom_add_multi_dev(c, filters, nseg, c->seg_offs.as<uint64_t>(), &kd, d_out, d_counts,
                                                c->stream);

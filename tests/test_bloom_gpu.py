@@ -295,8 +295,13 @@ def test_export_import_roundtrip(client, fresh):
     g.delete()
 
 
-def test_multi_tenant_parity(client, fresh):
+@pytest.mark.parametrize("small", [1, 0])
+def test_multi_tenant_parity(client, fresh, small):
+    """Multi-tenant add/contains from a host arena (segments in order, a tenant repeated), per key vs the
+    oracle; small 1: the one-transfer staging (counts, segment offsets and keys in one upload), 0: the
+    separate uploads."""
     rng = np.random.default_rng(12)
+    assert L.lib().rbx_tune(b"host_small_batches", small) == 0
     names = [f"{fresh}-{t}" for t in range(7)]
     shapes = [(14377587, 10), (729, 5), (9585, 7), (64, 7), (1000, 40), (1 << 20, 3), (100003, 17)]
     refs = []
@@ -320,6 +325,7 @@ def test_multi_tenant_parity(client, fresh):
         assert counts[s] == c
         assert np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl)
     probes_c, probes_f = bloom_contains_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
+    L.lib().rbx_tune(b"host_small_batches", 1)
     for s, t in enumerate(order):
         sub = keys[int(segs[s]):int(segs[s + 1])]
         c, fl = refs[t].contains(*O.arena(sub), per_key=True)

@@ -302,6 +302,17 @@ def main():
             }
             if nb == 1:
                 calls["contains_one_object"] = lambda i: fb.contains(bytes(hostkeys[0]))
+            if nb >= 4 and nb <= 4096:  # one multi-tenant host call over 4 filters (an RBatch of 4 collections)
+                from redisson_amd import bloom_add_multi, bloom_contains_multi
+
+                mh = []
+                for t in range(4):
+                    mf = client.getBloomFilter(f"sb-m{t}")
+                    mf.tryInit(1_000_000, 0.01)
+                    mh.append(BloomHandle(client, f"sb-m{t}"))
+                seg = np.array([0, nb // 4, nb // 2, 3 * nb // 4, nb], np.uint64)
+                calls["contains_multi4_host"] = lambda i: bloom_contains_multi(client, mh, seg, present)
+                calls["add_multi4_host"] = lambda i: bloom_add_multi(client, mh, seg, adds[i % 20])
             if nb <= 256:  # PFADD of nb host elements: a dense HLL, and a sparse one (a new HLL every 20 calls)
                 hd = client.getHyperLogLog(f"sb-hd-{nb}")
                 hd.addAll(Arena.fixed(rng.integers(0, 256, size=(200_000, 16), dtype=np.uint8)))
