@@ -240,6 +240,7 @@ struct rbx_ctx {
     // zeroed count word in one transfer; the count and flags come back into it
     void *pin_small = nullptr;
     size_t pin_small_cap = 0;
+    unsigned long long *pin_word = nullptr;  // pinned readback words (counts, the partitioned add's overflow flag)
 
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
     hipEvent_t ev_scratch = nullptr;
@@ -427,8 +428,10 @@ static int grow_bitmap(rbx_ctx *c, Bitmap &b, uint64_t size_bits, hipStream_t st
 
 static uint64_t read_dev_u64(rbx_ctx *c, const unsigned long long *p, int *rc) {
     unsigned long long v = 0;
-    hipError_t e = hipMemcpyAsync(&v, p, 8, hipMemcpyDeviceToHost, c->stream);
+    // into a pinned word: a pageable destination costs the runtime a staging copy
+    hipError_t e = hipMemcpyAsync(c->pin_word, p, 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) v = *c->pin_word;
     *rc = e == hipSuccess ? RBX_OK : fail(RBX_E_DEVICE, hipGetErrorString(e));
     return v;
 }
@@ -682,9 +685,10 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
         // the counters (but the mode word) and new_bits are zeroed by k_ba_mode, the chunk's first kernel
         launch_add_partitioned_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
-        uint32_t ovf = 0;
-        HIP_TRY(hipMemcpyAsync(&ovf, a.overflow, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->pin_word, a.overflow, 4, hipMemcpyDeviceToHost, st));  // pinned: no staging copy
         HIP_TRY(hipStreamSynchronize(st));
+        uint32_t ovf;
+        memcpy(&ovf, c->pin_word, 4);
         if (ovf) {
             // a bucket overflowed before any bitmap word changed: this chunk on the table path
             const KeysDev sub = keys_slice(keys, base, a.nchunk);
@@ -851,6 +855,7 @@ int rbx_init(int device, rbx_ctx **out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming);
         if (e == hipSuccess && i == 0) e = hipEventCreateWithFlags(&c->ev_scratch, hipEventDisableTiming);
     }
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->pin_word, 64, hipHostMallocDefault);
     if (e != hipSuccess) {
         delete c;
         return fail(RBX_E_DEVICE, hipGetErrorString(e));
@@ -913,6 +918,8 @@ int rbx_shutdown(rbx_ctx *c) {
         if (c->pin_small) (void)hipHostFree(c->pin_small);
         c->pin_small = nullptr;
         c->pin_small_cap = 0;
+        if (c->pin_word) (void)hipHostFree(c->pin_word);
+        c->pin_word = nullptr;
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->copy_stream = c->stream = nullptr;
