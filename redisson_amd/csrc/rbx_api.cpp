@@ -1707,6 +1707,9 @@ static uint32_t g_maddx_lgc = 17;
 // memory-side atomics), longer segments on the chunked path; 0 everything on the chunked path
 static int g_madd_seg = 1;
 static uint64_t g_madd_segmax = 16384;
+// rbx_tune("add_multi_seg_lgs"): log2 of the per-segment kernel's LDS table slots, 11 or 12 (a tile never
+// holds more than 2048 zero bits: tile x kmax <= 2048, so 2^11 slots never fill)
+static uint32_t g_madd_seg_lgs = 12;
 
 // Multi-tenant add on the 8-byte table: chunks of <= min(2^pb - 1, 2^27 / k) keys, each probe ->
 // final -> walk, in key order (a chunk's bits are set before the next probes).  The table and its
@@ -1802,7 +1805,7 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
         a.seg_off = d_seg_offsets;
         a.nseg = nseg;
         a.kmax = kmax;
-        a.lgs = 12;  // 4096 slots per table, 64 KiB of LDS: two workgroups per CU
+        a.lgs = g_madd_seg_lgs;  // 2^lgs slots per table, 16 B each (12: 64 KiB of LDS, two workgroups per CU)
         a.tile = std::max<uint32_t>(64, std::min<uint32_t>(256, (2048 / std::max<uint32_t>(kmax, 1)) & ~63u));
         a.segmax = g_madd_segmax;
         a.out_new = d_out_new;
@@ -3588,6 +3591,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_region_kernel")) {
         if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_kernel in {1, 2}");
         set_add_region_kernel(value);
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_multi_seg_lgs")) {
+        if (value != 11 && value != 12) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_seg_lgs in {11, 12}");
+        g_madd_seg_lgs = (uint32_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "host_small_bytes")) {

@@ -388,11 +388,12 @@ def test_multi_tenant_add_first_setter_tables(client, fresh, table8, clog2, chun
 
 
 ADD_MULTI_DEFAULT = 2
+ADD_MULTI_SEG_LGS_DEFAULT = 12
 
 
-@pytest.mark.parametrize("segmax", [16384, 300, 1])
+@pytest.mark.parametrize("segmax,lgs", [(16384, 12), (300, 12), (1, 12), (16384, 11)])
 @pytest.mark.parametrize("fixed", [True, False])
-def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
+def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, lgs, fixed):
     """r05: a multi-tenant add whose filters are all distinct runs one workgroup per segment (k_madd_seg:
     LDS first setters, plain word stores, tiles of <= 256 keys in order); segments longer than
     add_multi_segmax keys go to the chunked path in the same call (segmax 300: both paths; 1: every
@@ -423,6 +424,7 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
         keys = [pool[int(j)] for j in rng.integers(0, len(pool), size=n)]
         arena, sub = Arena(keys), (lambda a, b: O.arena(keys[a:b]))
     assert L.lib().rbx_tune(b"add_multi_segmax", segmax) == 0
+    assert L.lib().rbx_tune(b"add_multi_seg_lgs", lgs) == 0  # 11: 2^11 LDS slots, full at tile x kmax = 2048
     try:
         for rep in range(2):
             counts, flags = bloom_add_multi(client, handles, segs, arena, per_key=True)
@@ -434,6 +436,7 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, fixed):
                 assert int(counts.sum()) > n // 4
     finally:
         L.lib().rbx_tune(b"add_multi_segmax", 16384)
+        L.lib().rbx_tune(b"add_multi_seg_lgs", ADD_MULTI_SEG_LGS_DEFAULT)
     for nm, r in zip(names, refs):
         assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
     for h in handles:
