@@ -1130,10 +1130,27 @@ static uint64_t g_small_bytes = 4 << 20;  // rbx_tune("host_small_bytes"): the b
 static constexpr uint64_t kSmallHead = 64 << 10;  // zeroed result area ahead of the keys (counts, changed words)
 static size_t small_pin_bytes() { return kSmallHead + g_small_bytes + g_small_bytes / 4 + 64; }  // head | keys | tail
 
-static bool bloom_small_fits(const rbx_keys *k) {
-    if (k->n == 0 || k->n > g_small_bytes / 4) return false;
+// the pinned block of the one-transfer path, (re)allocated for the current limit; false (the caller takes
+// the pipelined path) when pinned memory cannot be had
+static bool small_pinned(rbx_ctx *c) {
+    const size_t pin = small_pin_bytes();
+    if (c->pin_small_cap >= pin) return true;
+    if (c->pin_small) (void)hipHostFree(c->pin_small);
+    c->pin_small = nullptr;
+    c->pin_small_cap = 0;
+    if (hipHostMalloc(&c->pin_small, pin, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        c->pin_small = nullptr;
+        return false;
+    }
+    c->pin_small_cap = pin;
+    return true;
+}
+
+static bool bloom_small_fits(rbx_ctx *c, const rbx_keys *k) {
+    if (!g_small_host || k->n == 0 || k->n > g_small_bytes / 4) return false;
     const uint64_t nb = k->offsets ? k->offsets[k->n] - k->offsets[0] : k->n * k->stride;
-    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= g_small_bytes;
+    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= g_small_bytes && small_pinned(c);
 }
 
 // One-transfer staging of a small host arena (bloom_small_fits): pinned [0, head) zeroed, the key bytes
@@ -1146,14 +1163,7 @@ struct SmallStage {
 };
 static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallStage *s, const void *head_src = nullptr,
                        uint64_t head_src_at = 0, uint64_t head_src_len = 0) {
-    const size_t pin = small_pin_bytes();
-    if (c->pin_small_cap < pin) {
-        if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
-        c->pin_small = nullptr;
-        c->pin_small_cap = 0;
-        HIP_TRY(hipHostMalloc(&c->pin_small, pin, hipHostMallocDefault));
-        c->pin_small_cap = pin;
-    }
+    const size_t pin = small_pin_bytes();  // allocated by bloom_small_fits (small_pinned)
     head = (std::max<uint64_t>(head, 8) + 63) / 64 * 64;  // <= kSmallHead (callers bound it)
     uint8_t *hp = (uint8_t *)c->pin_small;
     const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
@@ -1234,7 +1244,7 @@ static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint
         return RBX_OK;
     }
     FilterDesc f = desc_of(*bm, size_bits(size), k, 0);
-    if (g_small_host && bloom_small_fits(keys)) return bloom_host_small(c, f, k, keys, out_flags, out_count, is_add);
+    if (bloom_small_fits(c, keys)) return bloom_host_small(c, f, k, keys, out_flags, out_count, is_add);
     RBX_TRY(c->counters.reserve(64));
     auto *d_count = c->counters.as<unsigned long long>();
     HIP_TRY(hipMemsetAsync(d_count, 0, 8, c->stream));
@@ -1888,7 +1898,10 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     if (t8) RBX_TRY(c->st_fslot.reserve(chunk * 4));
     const uint32_t pbits = g_stream_prefilter ? (uint32_t)g_stream_prefilter : 20u;
     const uint64_t kPrefilterWords = 1ULL << (pbits - 5);
-    RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64) * 4));  // prefilter words + the add counter
+    // prefilter words, then one add counter per chunk (zeroed once per call: one fill, not one per chunk)
+    const uint64_t nchunks = (keys.n + chunk - 1) / chunk;
+    RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64 + nchunks) * 4));
+    HIP_TRY(hipMemsetAsync(c->st_prefilter.as<uint32_t>() + kPrefilterWords, 0, nchunks * 4, st));
     const int fl = fast_len(keys);
     if (t8) {
         const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)(k * g_stream_table_scale));
@@ -1930,13 +1943,12 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             s.fslot = c->st_fslot.as<uint32_t>();
         }
         s.adds = c->st_adds.as<uint32_t>();
-        s.nadds = c->st_prefilter.as<uint32_t>() + kPrefilterWords;
+        s.nadds = c->st_prefilter.as<uint32_t>() + kPrefilterWords + base / chunk;
         if (g_stream_prefilter) {
-            HIP_TRY(hipMemsetAsync(c->st_prefilter.p, 0, (kPrefilterWords + 1) * 4, st));
+            HIP_TRY(hipMemsetAsync(c->st_prefilter.p, 0, kPrefilterWords * 4, st));
             s.prefilter = c->st_prefilter.as<uint32_t>();
             s.pshift = 64 - pbits;
         } else {
-            HIP_TRY(hipMemsetAsync(s.nadds, 0, 4, st));
             s.prefilter = nullptr;
             if (t8 && g_stream_occ) {  // the table's slot-occupancy bitmap (k_stream_occ), pshift 0
                 s.prefilter = c->st_occ.as<uint32_t>();
@@ -2020,7 +2032,7 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
     ScratchOrder so_(c, c->stream);
     uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
     for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
-    if (g_small_host && (uint64_t)nseg * 16 + 8 <= kSmallHead && bloom_small_fits(keys)) {
+    if ((uint64_t)nseg * 16 + 8 <= kSmallHead && bloom_small_fits(c, keys)) {
         // one transfer: the zeroed per-segment counts, the segment offsets, the keys (bloom_host_small)
         SmallStage sm;
         const uint64_t so_at = (uint64_t)nseg * 8;
@@ -2245,7 +2257,7 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         created[s] = cr;
     }
     std::vector<uint32_t> ch(nseg);
-    if (g_small_host && nseg <= kSmallHead / 4 && bloom_small_fits(elements)) {
+    if (nseg <= kSmallHead / 4 && bloom_small_fits(c, elements)) {
         // one transfer for the elements and the zeroed changed words, one readback (bloom_host_small)
         SmallStage sm;
         RBX_TRY(small_stage(c, elements, nseg * 4, &sm));
