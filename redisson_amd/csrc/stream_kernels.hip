@@ -134,27 +134,33 @@ __device__ __forceinline__ bool maybe_claimed(const uint32_t *__restrict__ filte
 }
 
 // adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
+constexpr uint32_t kCompactPer = 64, kCompactBlock = 256 * kCompactPer;  // commands per lane / per block
 __global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restrict__ op, uint64_t base, uint64_t nchunk,
                                                         uint32_t *__restrict__ adds, uint32_t *__restrict__ nadds) {
-    // One pass, 4096 commands per block, 16 consecutive per lane: a block scan of the lanes'
-    // add counts and ONE reservation per block.  (A reservation per 1024-command tile, or a
-    // block walking a long slice, left the kernel latency-bound: 79 / 38 us for 6.7M commands.)
+    // One pass, kCompactBlock commands per block, kCompactPer consecutive per lane: a block scan of the
+    // lanes' add counts and ONE reservation per block.  The reservations of a chunk all go to one
+    // counter, which serialises them (~88 per us): 4096-command blocks -- 2K reservations per 8.4M-command
+    // chunk -- took 33 us a chunk; 16K-command blocks take a quarter of them (r05).  (A reservation per
+    // 1024-command tile, or a block walking a long slice, left the kernel latency-bound: 79 / 38 us for
+    // 6.7M commands.)
     __shared__ uint32_t s_w[4], s_base;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t t0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
-    uint32_t bits = 0;
-    if (t0 + 16 <= nchunk && ((base + t0) & 15) == 0) {  // the lane's 16 op bytes in one load (r05)
+    const uint64_t t0 = (uint64_t)blockIdx.x * kCompactBlock + threadIdx.x * kCompactPer;
+    uint64_t bits = 0;
+    if (t0 + kCompactPer <= nchunk && ((uintptr_t)(op + base + t0) & 15) == 0) {  // 16 op bytes per load
         using u8x16v = uint8_t __attribute__((ext_vector_type(16)));
-        const u8x16v v = *(const u8x16v *)(op + base + t0);
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if (v[q]) bits |= 1u << q;
+        for (uint32_t g = 0; g < kCompactPer / 16; ++g) {
+            const u8x16v v = *(const u8x16v *)(op + base + t0 + 16 * g);
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (v[q]) bits |= 1ULL << (16 * g + q);
+        }
     } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if (t0 + q < nchunk && op[base + t0 + q]) bits |= 1u << q;
+        for (uint32_t q = 0; q < kCompactPer; ++q)
+            if (t0 + q < nchunk && op[base + t0 + q]) bits |= 1ULL << q;
     }
-    const uint32_t c = (uint32_t)__popc(bits);
+    const uint32_t c = (uint32_t)__popcll(bits);
     uint32_t x = c;  // inclusive scan over the wave
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(256) void k_stream_compact(const uint8_t *__restric
     uint32_t pos = s_base + x - c;
     for (uint32_t w = 0; w < wave; ++w) pos += s_w[w];
     while (bits) {
-        adds[pos++] = (uint32_t)(t0 + (uint32_t)(__ffs(bits) - 1));
+        adds[pos++] = (uint32_t)(t0 + (uint32_t)(__ffsll((unsigned long long)bits) - 1));
         bits &= bits - 1;
     }
 }
@@ -1199,7 +1205,7 @@ void set_walk_reset_all(int v) { g_walk_reset_all = (uint32_t)v; }
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(a.nchunk, kMaxGrid);
-    const unsigned cgrid = (unsigned)((a.nchunk + 4095) / 4096);
+    const unsigned cgrid = (unsigned)((a.nchunk + kCompactBlock - 1) / kCompactBlock);
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
     const bool own8 = a.t8 && g_stream_owner == 1;  // r05: replies from the first claims, no flags
