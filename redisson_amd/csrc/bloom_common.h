@@ -43,6 +43,24 @@ __device__ __forceinline__ void block_add_u64(uint64_t v, unsigned long long *ds
     }
 }
 
+// the block's total stored (plain store, thread 0) at *dst -- a per-block partial that one small kernel
+// adds up afterwards (k_add_partials): same-address atomics from every block of a short kernel serialise
+// at its end (~140 per us measured on the stream's final kernel, r05as)
+__device__ __forceinline__ void block_store_u64(uint64_t v, unsigned long long *dst) {
+    __shared__ unsigned long long s_part[8];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) s_part[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        const int nw = (blockDim.x + 63) >> 6;
+        for (int w = 0; w < nw; ++w) t += s_part[w];
+        *dst = t;
+    }
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

@@ -108,7 +108,8 @@ template <int KLEN, int KMAX, int S1>
 __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint32_t *__restrict__ bm,
                                                         ModParams mp, uint32_t k,
                                                         uint8_t *__restrict__ out,
-                                                        unsigned long long *__restrict__ count) {
+                                                        unsigned long long *__restrict__ count,
+                                                        unsigned long long *__restrict__ partials) {
     uint64_t present = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < keys.n; i += stride) {
@@ -118,7 +119,16 @@ __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint
         if (out) out[i] = p;
         present += p;
     }
-    if (count) block_add_u64(present, count);
+    if (partials) block_store_u64(present, partials + blockIdx.x);  // summed by k_add_partials
+    else if (count) block_add_u64(present, count);
+}
+
+// *count += the n per-block partials (one block; one atomic)
+__global__ __launch_bounds__(256) void k_add_partials(const unsigned long long *__restrict__ partials, uint32_t n,
+                                                      unsigned long long *__restrict__ count) {
+    uint64_t v = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) v += partials[i];
+    block_add_u64(v, count);
 }
 
 // tile_seg0[t] = segment of key t*256 (one parallel binary search per 256-key tile)
@@ -653,8 +663,11 @@ int get_contains_stage1() { return g_stage1; }
 
 template <int KLEN, int KMAX, int S1>
 static void launch_contains_s(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
-    hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
+                              unsigned long long *partials = nullptr) {
+    unsigned long long *pp = count ? partials : nullptr;
+    hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count, pp);
+    if (pp) hipLaunchKernelGGL(k_add_partials, dim3(1), dim3(256), 0, st, pp, grid, count);
 }
 
 static unsigned g_qgrid = 2048;  // slot kernel grid (grid-stride over 64*Q-key ranges)
@@ -685,7 +698,8 @@ static void launch_contains_q(const KeysDev &keys, const FilterDesc *filt, const
 
 template <int KLEN, int KMAX>
 static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
+                               unsigned long long *partials) {
     if (g_stage1 == 5 && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
         FilterDesc f{};
         f.bm = const_cast<uint32_t *>(bm);
@@ -695,30 +709,32 @@ static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const Mo
         return;
     }
     switch (g_stage1) {
-    case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid); break;
-    case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid); break;
-    case 3: launch_contains_s<KLEN, KMAX, 3>(keys, bm, mp, k, out, count, st, grid); break;
-    case 4: launch_contains_s<KLEN, KMAX, 4>(keys, bm, mp, k, out, count, st, grid); break;
-    default: launch_contains_s<KLEN, KMAX, 1>(keys, bm, mp, k, out, count, st, grid); break;
+    case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 3: launch_contains_s<KLEN, KMAX, 3>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 4: launch_contains_s<KLEN, KMAX, 4>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    default: launch_contains_s<KLEN, KMAX, 1>(keys, bm, mp, k, out, count, st, grid, partials); break;
     }
 }
 
 template <int KLEN>
 static void launch_contains_k(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
-    if (k <= 8) launch_contains_km<KLEN, 8>(keys, bm, mp, k, out, count, st, grid);
-    else if (k <= 16) launch_contains_km<KLEN, 16>(keys, bm, mp, k, out, count, st, grid);
-    else launch_contains_s<KLEN, 0, 0>(keys, bm, mp, k, out, count, st, grid);
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
+                              unsigned long long *partials) {
+    if (k <= 8) launch_contains_km<KLEN, 8>(keys, bm, mp, k, out, count, st, grid, partials);
+    else if (k <= 16) launch_contains_km<KLEN, 16>(keys, bm, mp, k, out, count, st, grid, partials);
+    else launch_contains_s<KLEN, 0, 0>(keys, bm, mp, k, out, count, st, grid, partials);
 }
 
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
-                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st) {
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st,
+                           unsigned long long *partials) {
     const unsigned grid = grid_for(keys.n, kMaxGrid);
     switch (klen_fast) {
-    case 16: launch_contains_k<16>(keys, bm, mp, k, out, count, st, grid); break;
-    case 32: launch_contains_k<32>(keys, bm, mp, k, out, count, st, grid); break;
-    case 64: launch_contains_k<64>(keys, bm, mp, k, out, count, st, grid); break;
-    default: launch_contains_k<0>(keys, bm, mp, k, out, count, st, grid); break;
+    case 16: launch_contains_k<16>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 32: launch_contains_k<32>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 64: launch_contains_k<64>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    default: launch_contains_k<0>(keys, bm, mp, k, out, count, st, grid, partials); break;
     }
 }
 

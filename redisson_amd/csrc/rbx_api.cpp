@@ -235,6 +235,7 @@ struct rbx_ctx {
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf slot_bytes[2], slot_offs[2];
+    DevBuf partials;  // per-block counts of the direct contains kernel (contains_partials)
     uint64_t staging_bytes = 64ull << 20;
     // small host batches (bloom_host_small): a pinned copy of the keys, uploaded on `stream` with the
     // zeroed count word in one transfer; the count and flags come back into it
@@ -715,6 +716,10 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
 static int g_partition_mode = 2;
 static int g_partition_flags = 0;
 
+// rbx_tune("contains_partials"): 1 = the direct contains kernel stores per-block counts that one small kernel
+// adds up, 0 = one atomic per block into the count (they serialise at the kernel's end)
+static int g_contains_partials = 0;
+
 static bool use_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 2 || k > 16 || size > (1ULL << 32)) return false;
     if (g_partition_mode == 0) return false;
@@ -804,7 +809,12 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
 static int run_contains(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,
                         unsigned long long *d_count, hipStream_t st) {
     if (use_partitioned(f.mp.size, f.k, keys.n)) return run_contains_partitioned(c, keys, f, d_out, d_count, st);
-    launch_bloom_contains(keys, fast_len(keys), f.bm, f.mp, f.k, d_out, d_count, st);
+    unsigned long long *partials = nullptr;
+    if (g_contains_partials && d_count) {  // per-block counts + one summing launch (see launch_bloom_contains)
+        RBX_TRY(c->partials.reserve(kMaxGrid * 8));
+        partials = c->partials.as<unsigned long long>();
+    }
+    launch_bloom_contains(keys, fast_len(keys), f.bm, f.mp, f.k, d_out, d_count, st, partials);
     HIP_TRY(hipGetLastError());
     return RBX_OK;
 }
@@ -903,7 +913,7 @@ int rbx_shutdown(rbx_ctx *c) {
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
                           &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
                           &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot, &c->madd_c}) {
+                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot, &c->madd_c, &c->partials}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -3608,6 +3618,16 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "add_multi_seg_lgs")) {
         if (value != 11 && value != 12) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_seg_lgs in {11, 12}");
         g_madd_seg_lgs = (uint32_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "contains_partials")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partials in {0, 1}");
+        g_contains_partials = value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "stream_final_grid")) {
+        if (value < 32 || value > 2048) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_final_grid in [32, 2048]");
+        set_stream_final_grid(value);
         return RBX_OK;
     }
     if (!strcmp(key, "host_small_bytes")) {

@@ -234,8 +234,11 @@ __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
 
 // bloom_kernels.hip
 void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st);
+// partials (kMaxGrid words of scratch, or null): per-block counts summed by one small kernel instead of
+// one atomic per block into *count (short kernels: those atomics serialise at the end)
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
-                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st,
+                           unsigned long long *partials = nullptr);
 // tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)
 void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
@@ -275,6 +278,7 @@ void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kern
 void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
 void set_stream_probe_batch(int v);
 void set_stream_diag(int v);
+void set_stream_final_grid(int v);  // k_stream_final8 blocks (32..2048)
 void set_stream_owner(int v);          // 1 (default) replies from first-claim slots, 0 r04 owner flags
 void set_stream_lookup_rounds(int v);
 void set_walk_reset_all(int v);        // bit 0: stream walk, bit 1: multi-tenant add walk (whole-line resets)  // 1 (default) slot-kernel lookups as slot rounds, 0 inline  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip

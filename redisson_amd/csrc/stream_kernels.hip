@@ -1201,6 +1201,10 @@ void set_stream_lookup_rounds(int v) { g_stream_lookup_rounds = (uint32_t)v; }
 // the multi-tenant add's walk does
 static uint32_t g_walk_reset_all = 0;
 void set_walk_reset_all(int v) { g_walk_reset_all = (uint32_t)v; }
+// rbx_tune "stream_final_grid": k_stream_final8's blocks.  Each block adds its new-add count to ONE counter,
+// and same-address atomics serialise: 2048 / 512 / 256 blocks 39.3 / 28.3 / 35.6 us per C5 chunk (r05as).
+static unsigned g_final8_grid = 512;
+void set_stream_final_grid(int v) { g_final8_grid = (unsigned)v; }
 
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
@@ -1229,7 +1233,8 @@ static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
                            a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
                            a.t8, a.bb, a.pb, a.tkmax, a.nadds);
     if (own8) {
-        hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
+        hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(std::min(grid, g_final8_grid)), dim3(256), 0, st, a.keys,
+                           a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.zmask, a.fslot, a.out, a.counts);
         hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
                            (uint8_t *)nullptr, g_stream_diag, g_walk_reset_all & 1u);
