@@ -114,7 +114,12 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *   "contains_emit2_nt"     partitioned contains emit2 shape: 1536 (default: 1024 threads, 12K-pair
  *                           tiles), 1024 (8K-pair tiles), 1792 (14K), 512 (512 threads, 4K)
  *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather)
- *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048) */
+ *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048)
+ *   "add_multi_seg_lgs"     per-segment multi-tenant add: log2 of its LDS table slots, 12 (default) or 11
+ *   "stream_final_grid"     ordered stream: k_stream_final8 blocks, 32..2048 (default 512: each block
+ *                           adds its count to one counter, and those atomics serialise)
+ *   "contains_partials"     direct contains: 1 = per-block partial counts summed by one small launch,
+ *                           0 (default) = one count atomic per block */
 int rbx_tune(const char *key, int value);
 /* Test hook (fault injection): the next n Bloom adds that the node runs on GPU `gpu` (single or
  * multi-tenant, replica or home) fail with RBX_E_DEVICE before they touch the device; n = 0 clears.
