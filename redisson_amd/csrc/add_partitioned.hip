@@ -1226,8 +1226,9 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
-    // one thread per 32 keys (a per-thread chain over a smaller grid was the C1 add's third-largest cost)
-    hipLaunchKernelGGL(k_ba_final, dim3((unsigned)std::min<uint64_t>(2048, ((a.nchunk + 31) / 32 + 255) / 256)),
+    // one thread per 32 keys (a per-thread chain over a smaller grid was the C1 add's third-largest cost);
+    // at most 512 blocks: each adds its count to ONE counter, and those atomics serialise (r05)
+    hipLaunchKernelGGL(k_ba_final, dim3((unsigned)std::min<uint64_t>(512, ((a.nchunk + 31) / 32 + 255) / 256)),
                        dim3(256), 0, st, a.new_bits, a.ctr, a.f.k, a.nchunk, a.base, a.out_new, a.count, a.overflow,
                        a.mode);
 }

@@ -100,9 +100,11 @@ struct PcArgs {
     uint32_t flags;  // diagnostics only (rbx_tune "contains_partition_flags"); 0 in normal operation
     unsigned long long *stamps;  // flags & 64: emit2 / probe phase times (rbx_bench_add_stamps), else null
 };
+// k_bk_final's blocks: each adds its count to ONE counter, and same-address atomics serialise at the
+// kernel's end, so 512 blocks (grid-stride) rather than 2048 (r05, cf. k_stream_final8)
 inline unsigned grid_for_pc(uint64_t n) {
     uint64_t g = ((n + 63) / 64 + 255) / 256;
-    return (unsigned)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+    return (unsigned)(g < 1 ? 1 : (g > 512 ? 512 : g));
 }
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
 void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
