@@ -712,6 +712,13 @@ def run_c3(args, world, rank, local, steps, warmup):
     tbl = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
     peak = segment_gather_peak(client, tbl.data_ptr(), tbl.numel(), (size + 7) // 8, per, n, stream)
     del tbl
+    wpeak = stream_write_peak(client, 1 << 30, stream)
+    if add is not None:
+        # the add half against the same request roofline (reads at the segment-gather rate, writes at
+        # the stream-write rate): request_frac = its request floor / its call time
+        pipe, atj, ams = add.pop("_pipe"), add.pop("_tj"), add.pop("_ms")
+        if pipe:
+            add["roofline"].update(request_fields(atj, pipe, ams, peak, wpeak))
     algo = n * (16 + k * 8)
     achieved = algo / (ms / 1e3) / 1e9
     # PMC counts of profiles/traffic.json are of the default workload's calls only
@@ -735,7 +742,7 @@ def run_c3(args, world, rank, local, steps, warmup):
                      "traffic": load_traffic(tj, kname, "hbm_bytes_by_class") or load_traffic(tj, kname),
                      "kernel": kdesc, "kernel_avg_ms": ms,
                      "request_peak_kind": "k_gather_segments: 4 random loads per key inside its tenant's slice",
-                     **request_fields(tj, kname, ms, peak, stream_write_peak(client, 1 << 30, stream))},
+                     **request_fields(tj, kname, ms, peak, wpeak)},
         "extra": {"setup_s": setup_s, "present_fraction": present / n},
     }
     if add is not None:
@@ -792,17 +799,18 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
     tune = dict(kv.split("=") for kv in args.tune.split(",") if "=" in kv)
     mode, seg_path = tune.get("add_multi_table8", "2"), tune.get("add_multi_segment", "1") != "0"
     if mode == "2" and seg_path:  # every tenant of the batch distinct: one workgroup per segment
-        pipe, path = "k_madd_seg", "one workgroup per segment (k_madd_seg: LDS first setters, plain word stores)"
+        pipe = "k_madd_seg"
+        path = ("one workgroup per segment (k_madd_seg: tiles of <= 256 keys, LDS first setters, plain word "
+                "stores)")
     else:
-        pipe = {"1": "madd_pipeline", "0": None}.get(mode, "maddx_pipeline")
-        path = {"0": "16-byte epoch table (k_bloom_add_probe + commit)",
-                "1": "8-byte first-setter table (k_madd_probe8 + k_madd_final8 + k_stream_walk)"}.get(
-                    mode, "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)")
+        pipe = {"0": None}.get(mode, "maddx_pipeline")
+        path = {"0": "16-byte epoch table (k_bloom_add_probe + commit)"}.get(
+            mode, "optimistic SETBITs + conflict repair (k_maddx_gather + set + claim + reply)")
     del keys
     return {"metric": "Bloom add keys/sec (whole node), C3 tenants: one add(Collection) per tenant",
             "value": sum_over_ranks(world, n) / step_s, "unit": "keys/s", "ms_per_step": step_s * 1e3,
             "keys_per_gpu": n, "new_keys_per_step": new, "steps": steps, "warmup": warmup,
-            "path": path,
+            "path": path, "_pipe": pipe, "_tj": tj, "_ms": ms,
             "roofline": {"bound": "hbm", "achieved": algo / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": algo,
                          "traffic": load_traffic(tj, pipe, "hbm_bytes_by_class") if pipe else None,
@@ -815,7 +823,7 @@ def c3_add_half(args, client, arr, nt, per, k, seg, stream, g, steps, warmup, wo
 # C5: ordered 90/10 contains/add stream, Zipf(1.0) tenants over the C3 set, 64-byte keys
 # ------------------------------------------------------------------------------------------
 # the kernels one default C5 call runs per chunk (rbx_bloom_stream_dev with the default tuning)
-C5_KERNELS = "k_stream_compact + k_stream_probe8 + k_stream_contains_q + k_stream_walk + k_stream_final"
+C5_KERNELS = "k_stream_compact + k_stream_probe8 + k_stream_contains_q + k_stream_final8 + k_stream_walk"
 
 
 def run_c5(args, world, rank, local, steps, warmup):
@@ -949,22 +957,35 @@ def run_c4(args, world, rank, local, steps, warmup):
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     client = RedissonClient(local)
-    hs = []
-    for i in range(NH):
-        hp = C.c_void_p()
-        assert L.lib().rbx_hll_open(client.ctx, f"c4-{i}".encode(), 1, C.byref(hp)) == 0
-        hs.append(hp.value)
-    arr = (C.c_void_p * NH)(*hs)
+    # every step PFADDs fresh elements into 10k newly created HLLs (RedissonHyperLogLog
+    # .java:76-81 on keys that do not exist yet): each starts as Redis's sparse string and is promoted
+    # to dense inside the timed region, and every register update is a real change.  One set of 10k
+    # HLLs per (warmup + timed) step, all created before the timed region.
+    nsets = warmup + steps
+    sets = []
+    for j in range(nsets):
+        hs = []
+        for i in range(NH):
+            hp = C.c_void_p()
+            assert L.lib().rbx_hll_open(client.ctx, f"c4-{j}-{i}".encode(), 1, C.byref(hp)) == 0
+            hs.append(hp.value)
+        sets.append(hs)
+    arrs = [(C.c_void_p * NH)(*hs) for hs in sets]
     seg = np.arange(NH + 1, dtype=np.uint64) * np.uint64(per)
     g = torch.Generator(device="cuda")
     g.manual_seed(0x5EED0004 + rank)
-    el = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    # the element window slides by one HLL's share per step: HLL i of step j takes the elements HLL i + j
+    # took in step 0, so no (HLL, element) pair repeats
+    el = torch.randint(0, 256, (n + nsets * per, 16), dtype=torch.uint8, device="cuda", generator=g)
     changed = torch.zeros(NH, dtype=torch.int32, device="cuda")
-    dk = device_keys(el.data_ptr(), n, 16)
+    windows = [device_keys(el.data_ptr() + 16 * per * j, n, 16) for j in range(nsets)]
+    it = [0]
 
     def step():
-        assert L.lib().rbx_hll_add_multi_dev(client.ctx, arr, NH, None, seg.ctypes.data_as(L.u64p), C.byref(dk),
-                                             changed.data_ptr(), sptr) == 0
+        j = it[0]
+        it[0] += 1
+        assert L.lib().rbx_hll_add_multi_dev(client.ctx, arrs[j], NH, None, seg.ctypes.data_as(L.u64p),
+                                             C.byref(windows[j]), changed.data_ptr(), sptr) == 0
 
     for _ in range(warmup):
         step()
@@ -974,6 +995,8 @@ def run_c4(args, world, rank, local, steps, warmup):
         for _ in range(steps):
             step()
     ms = t.ms / steps
+    changed_last = int((changed != 0).sum().item())
+    arr = arrs[-1]
     del el
     nbytes = NH * 16384
     merge = {"allreduce_bytes": nbytes, "nranks_rccl": None, "rccl_max_allreduce_ms": None}
@@ -1034,7 +1057,8 @@ def run_c4(args, world, rank, local, steps, warmup):
         "value": value, "unit": "elems/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"C4 PFADD {per} x 16-byte elements into each of 10k HLLs per GPU",
+        "config": {"workload": f"C4 PFADD {per} fresh 16-byte elements into each of 10k newly created HLLs per "
+                               f"GPU per step (sparse -> dense promotion inside the timed region)",
                    "elements_per_gpu": n, "parallelism": f"element-partitioned x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
@@ -1044,10 +1068,12 @@ def run_c4(args, world, rank, local, steps, warmup):
                      "kernel": "k_hll_pfadd<16>", "kernel_avg_ms": ms,
                      # elems/s x 16 B / the measured HBM stream-read peak
                      "stream_read_peak_GBps": peak_gbs, "stream_frac": achieved / peak_gbs},
-        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean()), "merge": merge},
+        "extra": {"pfcount_10k_ms": count_ms, "mean_count": float(out.mean()), "merge": merge,
+                  "changed_replies_last_step": changed_last},
     }
-    for hp in hs:
-        L.lib().rbx_hll_close(hp)
+    for hs in sets:
+        for hp in hs:
+            L.lib().rbx_hll_close(hp)
     client.shutdown()
     torch.cuda.empty_cache()
     return res

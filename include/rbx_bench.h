@@ -23,7 +23,8 @@ int rbx_bench_gather_regions(rbx_ctx *ctx, const void *d_table, uint64_t table_b
 int rbx_bench_slice_probe(rbx_ctx *ctx, const void *d_entries, uint64_t per_bucket, uint32_t nbuckets,
                           const void *d_bitmap, uint64_t slice_bytes, unsigned grid, void *d_sink, void *stream);
 /* Region-pass phase times of the partitioned add, summed over every block's wave 0 since the
- * last read (s_memtime ticks; collected only while rbx_tune("add_partition_diag") has bit 64):
+ * last read (s_memtime ticks; collected only in the profiling build librbx_diag.so while
+ * rbx_tune("add_partition_diag") has bit 64; all zero in librbx.so):
  * copies n <= 16 counters to host `out` and zeroes them. */
 int rbx_bench_add_stamps(rbx_ctx *ctx, unsigned long long *out, uint32_t n);
 /* Stream-read roofline probe: reads `bytes` (16-byte aligned buffer) with 16-byte loads. */
@@ -41,85 +42,61 @@ int rbx_bench_gather_segments(rbx_ctx *ctx, const void *d_table, uint64_t table_
  * bits), out[2] = pb = 64 - bb - fbits (chunk-position bits; 0 when the 16-byte table ran),
  * out[3] = commands per chunk.  Tests pin the production packing with it. */
 int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
-/* Process-wide tuning knobs (results never change; A/B runs and tests only):
+/* Process-wide tuning knobs: the whole whitelist (r06).  No knob of librbx.so changes an answer: each
+ * selects between exact paths (the fallbacks the engine takes by itself on other shapes, forced so the
+ * tests cover them), or sets a grid, chunk or capacity.  Knobs are atomics; a call reads each once.
  *   "contains_stage1"       early-exit schedule of contains: 0 = all k gathers at once,
  *                           1..3 = that many bits first, 4 = doubling 1,2,4,... (default),
  *                           5 = per-lane key slots (one bit per key per round trip)
+ *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,
+ *                           2 auto (default: the call's bitmaps exceed 64 MiB)
+ *   "contains_qgrid"        slot contains kernel grid, 256..8192 (default 2048)
  *   "contains_partition"    region-bucketed contains for one large filter: 0 never, 1 always
  *                           (k in [2,16]), 2 auto (default: bitmap >= 256 MiB, >= 4M keys)
- *   "contains_partition_flags"  diagnostics of that pipeline: 0 (default), 4, 8, 12 (wrong
- *                           answers), 16 (exact: one atomicOr per clear bit, no miss records)
  *   "add_partition"         region-partitioned add: 0 never, 1 always, 2 auto (default:
  *                           bitmap >= 8 MiB and >= max(2^17, bits / 2^12) keys)
  *   "add_records"           how the partitioned add reports new keys: 0 owner bits, 1 non-owner
  *                           counters, 3 owner records, 2 (default) chosen from the sampled fill
- *   "add_partition_diag"    0 (default); bits 4|8|16 (diagnostics, wrong answers); 64 (exact:
- *                           region-pass phase times, read by rbx_bench_add_stamps)
- *   "add_region_kernel"     partitioned add region pass: 2 (default: 6-byte region pairs,
- *                           pipelined k_ba_region6), 1 (8-byte pairs, k_ba_region)
+ *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048)
+ *   "add_rec_lds_limit"     owner records a region block stages in LDS, 0..7168 (default 7168;
+ *                           tests use small limits to run the direct-report fallback)
+ *   "add_multi_table8"      multi-tenant add when (filter id, bit) fits 41 bits and k <= 32: 2 (default)
+ *                           optimistic SETBITs (returning atomicOr) with a small conflict table for the
+ *                           zero bits two keys share; 0 the 16-byte first-setter table (the fallback)
+ *   "add_multi_conflict_log2"  entries (log2, 6..24, default 17) of that conflict table; past half full
+ *                           the chunk's replies come from the full first-setter table
+ *   "add_multi_segment"     1 (default): a multi-tenant add whose filters are all distinct runs each
+ *                           segment of <= add_multi_segmax keys in one workgroup (k_madd_seg: tiles of
+ *                           <= 256 keys, LDS first setters, plain word stores), longer ones on the path
+ *                           above; 0: off
+ *   "add_multi_segmax"      that segment-length limit (keys, 1..16384)
+ *   "add_multi_seg_grid"    the per-segment kernel's workgroups, 64..65536 (default 8192), grid-stride
+ *                           over the segments
+ *   "stream_table8"         ordered stream's first-setter table: 1 (default) 8-byte entries claimed
+ *                           by one CAS and committed by a table walk, 0 the 16-byte epoch-tagged table
+ *                           (the fallback when (filter id, bit) does not fit 41 bits)
+ *   "stream_chunk"          commands per chunk cap (0 = default) of the ordered stream (default: with
+ *                           the 8-byte table min(2^pb - 1, 2^27 / k) rounded down to 128, else 2^26 / k)
+ *                           and of the chunked multi-tenant add (default min(2^pb - 1, 2^27 / k), not
+ *                           rounded)
+ *   "stream_qgrid"          ordered-stream slot contains kernel grid, 256..8192 (default 1024)
+ *   "stream_final_grid"     ordered stream: k_stream_final8 blocks, 32..2048 (default 512: each block
+ *                           adds its count to one counter, and those atomics serialise)
+ *   "wide_subchunk"         add / contains on a filter past 2^32 bits: keys per sub-chunk cap (0 =
+ *                           default 2^29 / k, which bounds the first-setter table at 2^30 entries)
  *   "host_small_batches"    1 (default): host-arena add/contains batches within host_small_bytes
  *                           take the one-transfer path (pinned copy, one upload, one readback);
  *                           0: every host batch on the pipelined copy-stream path
  *   "host_small_bytes"      that path's limit: key bytes (+ offsets), 4 KiB .. 64 MiB (default
  *                           4 MiB; at most a quarter as many keys)
- *   "add_rebucket_lines"    partitioned add rebucket: 0 (default) k_ba_rebucket, 1 k_ba_emit2
- *                           (whole-line region runs, LDS carries; measured 0.03 ms slower at C2),
- *                           2 k_ba_emit2 when a chunk has >= 1024 stage-1 partitions
- *   "add_rec_lds_limit"     owner records a region block stages in LDS, 0..7168 (default 7168;
- *                           tests use small limits to run the direct-report fallback)
- *   "contains_multi_slots"  multi-tenant contains with key slots: 0 never, 1 always,
- *                           2 auto (default: the call's bitmaps exceed 64 MiB)
- *   "contains_qshape"       slot kernel shape P*10+Q: 22 (default), 24, 32, 34, 42, 44
- *   "contains_qgrid"        slot kernel grid, 256..8192 (default 2048)
- *   "stream_contains_slots" ordered-stream contains: 1 slot kernel (default), 0 staged kernel
- *   "stream_table8"         ordered stream's first-setter table: 1 (default) 8-byte entries claimed
- *                           by one CAS and committed by a table walk, 0 the 16-byte epoch-tagged table
- *   "stream_prefilter"      ordered stream: 0 (default) every clear bit of a contains is looked up in
- *                           the first-setter table; 16..27 = a 2^bits prefilter of the adds' zero
- *                           bits gates the lookups (one atomicOr per zero bit)
- *   "stream_occupancy"      ordered stream without a prefilter, 8-byte table: 1 = lookups gated by
- *                           the occupancy bitmap of the table's slots, 0 (default) = none
- *   "add_multi_table8"      multi-tenant add when (filter id, bit) fits 41 bits and k <= 32: 2 (default)
- *                           optimistic SETBITs (returning atomicOr) with a small conflict table for the
- *                           zero bits two keys share, 1 the 8-byte first-setter table (claims by one CAS,
- *                           replies from the first claim's slot, walk commit), 0 the 16-byte epoch table
- *   "add_multi_segment"     1 (default): a multi-tenant add whose filters are all distinct runs each
- *                           segment of <= add_multi_segmax keys (default 16384) in one workgroup (LDS
- *                           first setters, plain word stores), longer ones on the path above; 0: off
- *   "add_multi_segmax"      that segment-length limit (keys, >= 1)
- *   "add_multi_conflict_log2"  entries (log2, 6..24, default 17) of the conflict table of mode 2; past
- *                           half full the chunk's replies come from the full first-setter table
- *   "walk_reset_all"        the 8-byte table's walk: bit 0 (ordered stream) / bit 1 (multi-tenant add)
- *                           rewrites every pair EMPTY with whole-line stores; clear: only occupied pairs
- *   "stream_chunk"          ordered stream and 8-byte multi-tenant add: commands per chunk cap (0 = default: with the 8-byte
- *                           table min(2^pb - 1, 2^27 / k) rounded down to 128, else 2^26 / k)
- *   "wide_subchunk"         add / contains on a filter past 2^32 bits: keys per sub-chunk cap (0 =
- *                           default 2^29 / k, which bounds the first-setter table at 2^30 entries)
- *   "stream_qgrid"          ordered-stream slot contains kernel grid, 256..8192 (default 1024)
- *   "stream_table_scale"    ordered stream, 8-byte table entries x 1 (default), 2 or 4
- *   "stream_probe_batch"    ordered stream, 8-byte table: 1 (default) an add's zero-bit claims (home-
- *                           slot CAS) all in flight at once, 0 one after another
- *   "stream_owner"          ordered stream, 8-byte table: 1 (default) add replies from the slot of each
- *                           add's first zero-bit claim (k_stream_final8, before the walk), 0 owner flags
- *                           written by the walk (r04)
- *   "stream_lookup_rounds"  ordered-stream slot contains, 8-byte table, no prefilter: 1 (default) a
- *                           first-setter lookup is a round of its slot, 0 looked up inline
- *   "stream_diag"           DIAGNOSTICS ONLY, answers become wrong (timing A/Bs): bits 1 = stream
- *                           contains skip the first-setter lookups, 2 = walk ORs with plain stores,
- *                           4 = walk writes no owner flags, 8 = probe makes no claims
- *   "stream_contains_lds"   dynamic LDS bytes per ordered-stream contains block, i.e. a cap on its
- *                           resident blocks (default 33000: four per CU; 0: registers decide)
- *   "contains_stage1_per"   partitioned contains stage 1, keys per thread for k <= 8: 2 (default,
- *                           1024-key tiles) or 1 (512-key tiles)
- *   "contains_emit2_nt"     partitioned contains emit2 shape: 1536 (default: 1024 threads, 12K-pair
- *                           tiles), 1024 (8K-pair tiles), 1792 (14K), 512 (512 threads, 4K)
- *   "contains_partition_flags" also takes 32 (diagnostics, wrong answers: no bit-0 gather)
- *   "add_region_grid"       partitioned add, region-pass blocks in [256, 65536] (default 2048)
- *   "add_multi_seg_lgs"     per-segment multi-tenant add: log2 of its LDS table slots, 12 (default) or 11
- *   "stream_final_grid"     ordered stream: k_stream_final8 blocks, 32..2048 (default 512: each block
- *                           adds its count to one counter, and those atomics serialise)
- *   "contains_partials"     direct contains: 1 = per-block partial counts summed by one small launch,
- *                           0 (default) = one count atomic per block */
+ * Profiling build only (librbx_diag.so, `make diag`; librbx.so rejects them): "stream_diag",
+ * "contains_partition_flags", "add_partition_diag" -- timing diagnostics that make answers wrong
+ * (rbx_kernels.h kDiag).  Removed in r06 with the variants they selected (measured slower, never
+ * default; the A/B records stay in profiles/): contains_qshape, contains_partials, contains_emit2_nt,
+ * contains_stage1_per, add_region_kernel, add_rebucket_lines, add_rebucket_prefetch,
+ * add_stage1_prefetch, add_multi_seg_lgs, stream_prefilter, stream_occupancy, stream_table_scale,
+ * stream_contains_slots, stream_contains_lds, stream_owner, stream_lookup_rounds, stream_probe_batch,
+ * walk_reset_all, add_multi_table8 1. */
 int rbx_tune(const char *key, int value);
 /* Test hook (fault injection): the next n Bloom adds that the node runs on GPU `gpu` (single or
  * multi-tenant, replica or home) fail with RBX_E_DEVICE before they touch the device; n = 0 clears.

@@ -32,6 +32,8 @@
 // either way.
 #include "bucket_common.h"
 
+#include <atomic>
+
 namespace rbx {
 
 constexpr uint32_t kBaRegionWords = 1u << (kBaRegionBits - 5);  // 2048
@@ -333,143 +335,8 @@ constexpr uint32_t kBaLine = 32;
 constexpr uint16_t kBaPadHi = 0xffffu;  // hi half of a padding pair: real keys are < 2^26 (hi < 1024)
 static_assert(kBaMaxRegionPairs <= 65536, "region pair counts fit the LDS counters");
 
-template <int PER, bool STAMP>
-__global__ __launch_bounds__(1024) void k_ba_emit2(const unsigned long long *__restrict__ pin,
-                                                   const uint32_t *__restrict__ cnt_in, uint64_t cap_in,
-                                                   uint32_t nparents, uint32_t sub_div, uint32_t shift_out, uint32_t fo,
-                                                   uint32_t nparts_out, unsigned long long *__restrict__ pout,
-                                                   uint32_t *__restrict__ cnt_out, uint64_t cap_out,
-                                                   uint32_t *__restrict__ overflow, unsigned long long *__restrict__ stamps) {
-    constexpr uint32_t NT = 1024, TILE = 2 * PER * NT;
-    PhaseStamps<STAMP, 4> ps;
-    ps.start();
-    __shared__ __attribute__((aligned(16))) unsigned long long s_img[TILE];
-    __shared__ uint32_t s_clo[256 * kBaLine];  // carried pairs: lo words
-    __shared__ uint16_t s_chi[256 * kBaLine];  // and hi halves
-    __shared__ uint32_t s_cnt2[2][256], s_start[256], s_pos[256], s_gb[256], s_full[256], s_cn[256];
-    const uint32_t nf = 1u << fo, fmask = nf - 1;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t nparts = nparents * sub_div;
-    auto lo_of = [](unsigned long long e) { return (uint32_t)(e >> 32) << 16 | ((uint32_t)e & 0xffffu); };
-    auto hi_of = [](unsigned long long e) { return (uint16_t)((uint32_t)e >> 16); };
-    // pair t of region r's run (whole lines: gb and every reservation are multiples of kBaLine)
-    auto put = [&](uint32_t r, uint64_t slot, uint32_t lo, uint16_t hi) {
-        if (slot < cap_out) {
-            uint32_t *plo = (uint32_t *)pout + (uint64_t)r * (cap_out * 3 / 2);
-            run_store(lo, plo + slot);
-            run_store(hi, (uint16_t *)(plo + cap_out) + slot);
-        } else {
-            *overflow = 1u;
-        }
-    };
-    for (uint32_t item = blockIdx.x; item < nparts; item += gridDim.x) {
-        // items parent-minor: the blocks running at one time reserve from different parents' regions
-        const uint32_t parent = item % nparents, part = parent * sub_div + item / nparents;
-        const uint64_t nc = min<uint64_t>(cnt_in[part], cap_in);
-        if (threadIdx.x < 256) {
-            s_cn[threadIdx.x] = 0;
-            s_cnt2[0][threadIdx.x] = 0;
-        }
-        uint32_t par = 0;
-        __syncthreads();
-        // cap_in is a multiple of 8192 pairs and TILE of 2048: every tile is 16-byte aligned
-        const u32x4 *src0 = (const u32x4 *)(pin + (uint64_t)part * cap_in);
-        u32x4 v[PER];  // the next tile, loaded while the current one is bucketed and written
-        auto load = [&](uint64_t st) {
-            const uint32_t mm = (uint32_t)min<uint64_t>(TILE, nc - st);
-#pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                v[p] = u32x4{0u, 0u, 0u, 0u};
-                if (2 * (p * NT + threadIdx.x) < mm) v[p] = __builtin_nontemporal_load(src0 + st / 2 + p * NT + threadIdx.x);
-            }
-        };
-        if (nc) load(0);
-        for (uint64_t start = 0; start < nc; start += TILE) {
-            const uint32_t m = (uint32_t)min<uint64_t>(TILE, nc - start);
-            uint32_t *s_cnt = s_cnt2[par];
-            if (threadIdx.x < 256) s_cnt2[par ^ 1][threadIdx.x] = 0;  // the next tile's (after this tile's last barrier)
-            unsigned long long e[2 * PER];
-#pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                e[2 * p] = w2(v[p].x, v[p].y);
-                e[2 * p + 1] = w2(v[p].z, v[p].w);
-            }
-#pragma unroll
-            for (int p = 0; p < 2 * PER; ++p) {
-                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
-                if (q < m) atomicAdd(&s_cnt[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u);
-            }
-            __syncthreads();
-            ps.mark(0);
-            // reservations issued here, their results stored after the placement (which hides the
-            // round trip); the next tile's loads follow them
-            uint32_t gb = 0;
-            if (threadIdx.x < 64) bk_scan256(s_cnt, nf, s_start, s_pos);
-            else if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) {
-                const uint32_t f = threadIdx.x - 256;
-                const uint32_t r = (parent << fo) + f;
-                const uint32_t full = (s_cn[f] + s_cnt[f]) & ~(kBaLine - 1);
-                s_full[f] = full;
-                if (full && r < nparts_out) gb = atomicAdd(&cnt_out[r], full);
-            }
-            if (start + TILE < nc) load(start + TILE);
-            __syncthreads();
-            ps.mark(1);
-#pragma unroll
-            for (int p = 0; p < 2 * PER; ++p) {
-                const uint32_t q = 2 * ((p >> 1) * NT + threadIdx.x) + (p & 1);
-                if (q < m) s_img[atomicAdd(&s_pos[(uint32_t)(e[p] >> (32 + shift_out)) & fmask], 1u)] = e[p];
-            }
-            if (threadIdx.x >= 256 && threadIdx.x - 256 < nf) s_gb[threadIdx.x - 256] = gb;
-            __syncthreads();
-            ps.mark(2);
-            // a wave per fine bucket: its carries then its new pairs, the whole lines out, the rest carried
-            for (uint32_t f = wave; f < nf; f += NT / 64) {
-                const uint32_t n = s_cnt[f], cn = s_cn[f], full = s_full[f], st = s_start[f];
-                const uint32_t r = (parent << fo) + f;
-                for (uint32_t t = lane; t < full; t += 64) {
-                    uint32_t lo;
-                    uint16_t hi;
-                    if (t < cn) {
-                        lo = s_clo[f * kBaLine + t];
-                        hi = s_chi[f * kBaLine + t];
-                    } else {
-                        const unsigned long long x = s_img[st + t - cn];
-                        lo = lo_of(x);
-                        hi = hi_of(x);
-                    }
-                    put(r, (uint64_t)s_gb[f] + t, lo, hi);
-                }
-                // full > 0 means full >= kBaLine > cn: every old carry went out above
-                const uint32_t rem = cn + n - full, from = full ? full - cn : 0u, to = full ? 0u : cn;
-                for (uint32_t t = lane; t < rem - to; t += 64) {
-                    const unsigned long long x = s_img[st + from + t];
-                    s_clo[f * kBaLine + to + t] = lo_of(x);
-                    s_chi[f * kBaLine + to + t] = hi_of(x);
-                }
-                if (lane == 0) s_cn[f] = rem;
-            }
-            par ^= 1u;
-            __syncthreads();
-            ps.mark(3);
-        }
-        for (uint32_t f = wave; f < nf; f += NT / 64) {  // the item's last remainders, padded to a line
-            const uint32_t cn = s_cn[f];
-            if (cn == 0) continue;  // uniform over the wave
-            const uint32_t r = (parent << fo) + f;
-            uint32_t gb = 0;
-            if (lane == 0) gb = atomicAdd(&cnt_out[r], kBaLine);
-            gb = __shfl(gb, 0, 64);
-            if (lane < kBaLine) {
-                if (lane < cn) put(r, (uint64_t)gb + lane, s_clo[f * kBaLine + lane], s_chi[f * kBaLine + lane]);
-                else put(r, (uint64_t)gb + lane, 0u, kBaPadHi);
-            }
-        }
-        __syncthreads();  // s_cn / carries reused by the next item
-        ps.mark(3);
-    }
-    ps.flush(stamps);
-}
+// (k_ba_emit2, the whole-line rebucket, measured 0.03 ms slower at C2 and was removed in r06:
+// profiles/r05/; the padding constants above stay for the region pass.)
 
 // mode -----------------------------------------------------------------------------------
 // Sampled fill of the bitmap -> how C reports new keys (see the header): 1 = non-owner counters,
@@ -533,178 +400,10 @@ __device__ __forceinline__ uint32_t ba_slot(uint32_t off, uint32_t t) {
     return ((off * 2654435761u) >> (32 - kBaTableBits)) + t & ((1u << kBaTableBits) - 1);
 }
 
-template <bool STAMP>
-__global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ba_region(
-    const unsigned long long *__restrict__ p3, const uint32_t *__restrict__ cnt3, uint64_t cap3, uint32_t nregions,
-    uint32_t *__restrict__ bm, uint64_t nwords4, uint32_t *__restrict__ new_bits, uint32_t *__restrict__ ctr,
-    uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt, uint64_t cap_rec, uint32_t nranges,
-    const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t diag,
-    unsigned long long *__restrict__ stamps) {
-    PhaseStamps<STAMP> ps;
-    constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, T = 1u << kBaTableBits;
-    constexpr uint32_t kOff = (1u << kBaRegionBits) - 1;
-    constexpr uint32_t NV = kBaRegionWords / 4;  // 16-byte vectors of the region
-    __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBaRegionWords];     // 8 KiB
-    __shared__ __attribute__((aligned(16))) uint32_t s_seen[kBaRegionWords];   // met at 0 by a pair
-    __shared__ __attribute__((aligned(16))) uint32_t s_multi[kBaRegionWords];  // met at 0 by >= 2 pairs
-    __shared__ uint32_t s_toff[T], s_tmin[T];                                  // 8 KiB
-    __shared__ uint32_t s_rec[kBaMaxRegionPairs];                              // owner records, 32 KiB
-    __shared__ uint32_t s_rc[64], s_rst[64], s_rpos[64], s_rgb[64];
-    static_assert(NV <= NT, "one u32x4 of the region per thread");
-    if (*overflow) return;
-    const uint32_t md = *mode;
-    const bool counters = md == 1, records = md == 2, bits = md == 0;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long e[PER];
-    bool loaded = false;
-    ps.start();
-    for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
-        const uint32_t n = (uint32_t)min<uint64_t>(cnt3[r], cap3);
-        if (n == 0) continue;  // uniform
-        const uint64_t w0 = (uint64_t)r * kBaRegionWords;
-        const bool vec = threadIdx.x < NV;
-        const bool has_words = vec && w0 + 4 * threadIdx.x < nwords4;  // nwords4 and w0 are multiples of 4
-        if (!(diag & 8) || !loaded) {                            // diag 8: loads of the first region only
-            const unsigned long long *src = p3 + (uint64_t)r * cap3;
-#pragma unroll
-            for (uint32_t p = 0; p < PER; ++p) {
-                const uint32_t q = p * NT + threadIdx.x;
-                e[p] = q < n ? __builtin_nontemporal_load(src + q) : 0ULL;
-            }
-            loaded = true;
-        }
-        u32x4 bw = {0u, 0u, 0u, 0u};
-        if (has_words) bw = ((const u32x4 *)(bm + w0))[threadIdx.x];
-        if (diag & 16) {  // diagnostics: loads only
-            unsigned long long acc = bw.x ^ bw.w;
-#pragma unroll
-            for (uint32_t p = 0; p < PER; ++p) acc ^= e[p];
-            if (acc == 0x9e3779b97f4a7c15ULL) bm[0] = 0u;
-            continue;
-        }
-        if (vec) {
-            ((u32x4 *)s_bm)[threadIdx.x] = bw;
-            ((u32x4 *)s_seen)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
-            ((u32x4 *)s_multi)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
-        }
-        for (uint32_t i = threadIdx.x; i < T; i += NT) {
-            s_toff[i] = ~0u;
-            s_tmin[i] = ~0u;
-        }
-        if (threadIdx.x < 64) s_rc[threadIdx.x] = 0;
-        __syncthreads();
-        ps.mark(0);
-        // pass 1: which pairs meet a 0 bit, and which of those bits are met more than once
-        uint32_t zm = 0;
-#pragma unroll
-        for (uint32_t p = 0; p < PER; ++p) {
-            const uint32_t idx = (uint32_t)(e[p] >> 32), w = (idx & kOff) >> 5, b = bit_in_word(idx);
-            if (p * NT + threadIdx.x < n && (s_bm[w] & b) == 0u) {
-                zm |= 1u << p;
-                if (atomicOr(&s_seen[w], b) & b) atomicOr(&s_multi[w], b);
-            }
-        }
-        __syncthreads();
-        ps.mark(3);
-        // pass 2: a bit met once is owned by its pair; bits met again go through the table
-        uint32_t own = 0, pend = 0;
-#pragma unroll
-        for (uint32_t p = 0; p < PER; ++p) {
-            if (zm & (1u << p)) {
-                const uint32_t idx = (uint32_t)(e[p] >> 32);
-                if (s_multi[(idx & kOff) >> 5] & bit_in_word(idx)) pend |= 1u << p;
-                else own |= 1u << p;
-            }
-        }
-        ps.mark(4);
-        bool first = true;
-        while (__syncthreads_or(pend != 0u)) {  // uniform; also orders the previous round's reads
-            if (!first) {
-                for (uint32_t i = threadIdx.x; i < T; i += NT) {
-                    s_toff[i] = ~0u;
-                    s_tmin[i] = ~0u;
-                }
-                __syncthreads();
-            }
-            first = false;
-            uint32_t ins = 0;
-#pragma unroll
-            for (uint32_t p = 0; p < PER; ++p) {
-                if (pend & (1u << p)) {
-                    const uint32_t off = (uint32_t)(e[p] >> 32) & kOff, key = (uint32_t)e[p];
-                    for (uint32_t t = 0; t < 64; ++t) {
-                        const uint32_t sl = ba_slot(off, t);
-                        const uint32_t cur = atomicCAS(&s_toff[sl], ~0u, off);
-                        if (cur == ~0u || cur == off) {
-                            atomicMin(&s_tmin[sl], key);
-                            ins |= 1u << p;
-                            break;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t p = 0; p < PER; ++p) {
-                if (ins & (1u << p)) {  // found again along the same probe sequence
-                    const uint32_t off = (uint32_t)(e[p] >> 32) & kOff, key = (uint32_t)e[p];
-                    uint32_t sl = ba_slot(off, 0);
-                    for (uint32_t t = 1; s_toff[sl] != off; ++t) sl = ba_slot(off, t);
-                    if (s_tmin[sl] == key) own |= 1u << p;
-                }
-            }
-            pend &= ~ins;  // bits not inserted this round (table full) retry with a cleared table
-        }
-        ps.mark(5);
-        // owners set their bits; the other kind is reported to the key pass
-#pragma unroll
-        for (uint32_t p = 0; p < PER; ++p) {
-            const uint32_t idx = (uint32_t)(e[p] >> 32), key = (uint32_t)e[p];
-            if (own & (1u << p)) {
-                atomicOr(&s_bm[(idx & kOff) >> 5], bit_in_word(idx));
-                if (diag & 4) continue;
-                if (bits) atomicOr(&new_bits[key >> 5], 1u << (key & 31));
-                else if (records) atomicAdd(&s_rc[key >> kBaKeyRangeBits], 1u);
-            } else if (counters && !(diag & 4) && p * NT + threadIdx.x < n) {
-                atomicAdd(&ctr[key >> 2], 1u << (8 * (key & 3)));  // no return: not waited on here
-            }
-        }
-        const bool changed = __syncthreads_or(own != 0u);
-        ps.mark(6);
-        if (!changed) continue;  // uniform: no bit changed
-        if (has_words) ((u32x4 *)(bm + w0))[threadIdx.x] = ((const u32x4 *)s_bm)[threadIdx.x];
-        if (records && !(diag & 4)) {  // uniform: owner key ids as runs per 2^20-key range
-            uint32_t gb = 0;
-            const uint32_t q = threadIdx.x - 128;
-            const bool reserver = threadIdx.x >= 128 && q < nranges;
-            if (threadIdx.x < 64) bk_scan128(s_rc, nranges, s_rst, s_rpos);
-            else if (reserver && s_rc[q]) gb = atomicAdd(&rec_cnt[q], s_rc[q]);
-            __syncthreads();
-#pragma unroll
-            for (uint32_t p = 0; p < PER; ++p) {
-                if (own & (1u << p)) {
-                    const uint32_t key = (uint32_t)e[p];
-                    s_rec[atomicAdd(&s_rpos[key >> kBaKeyRangeBits], 1u)] = key;
-                }
-            }
-            if (reserver) s_rgb[q] = gb;
-            __syncthreads();
-            // records per range <= 2^20 keys x k = cap_rec: no overflow
-            for (uint32_t rq = wave; rq < nranges; rq += NT / 64) {
-                const uint32_t rn = s_rc[rq], st = s_rst[rq];
-                uint32_t *dst = recs + (uint64_t)rq * cap_rec + s_rgb[rq];
-                for (uint32_t t = lane; t < rn; t += 64) run_store(s_rec[st + t], dst + t);
-            }
-        }
-        __syncthreads();  // s_bm / s_rec reuse
-        ps.mark(7);
-    }
-    ps.flush(stamps);
-}
 
 // C (6-byte pairs, pipelined) -----------------------------------------------------------
-// The same resolution as k_ba_region, with the next region's inputs in flight while the current
-// one is resolved.  k_ba_region waited, per region, for its pair count, then for the region's pairs
+// The region pass (the resolution of the r02 k_ba_region, removed in r06), with the next region's inputs in flight while the current
+// one is resolved.  The r02 kernel waited, per region, for its pair count, then for the region's pairs
 // and bitmap (two dependent memory round trips before any work), and took 60 B/lane of spills.
 // Here, right after a region's pairs are copied from LDS into registers, the block issues the next
 // region's pairs straight into that LDS buffer (global_load_lds: no registers held for them) and
@@ -769,6 +468,7 @@ __global__ __launch_bounds__(kBaRegionThreads) __attribute__((amdgpu_waves_per_e
     uint32_t *__restrict__ recs, uint32_t *__restrict__ rec_cnt, uint64_t cap_rec, uint32_t nranges,
     const uint32_t *__restrict__ overflow, const uint32_t *__restrict__ mode, uint32_t rec_limit, uint32_t diag,
     unsigned long long *__restrict__ stamps) {
+    if (!kDiag) diag = 0;  // wrong-answer diagnostics exist in the profiling build only (rbx_kernels.h)
     constexpr uint32_t NT = kBaRegionThreads, PER = kBaPer, C = kBa6Slots;
     PhaseStamps<STAMP> ps;
     constexpr uint32_t NV = kBaRegionWords / 4;  // 16-byte vectors of the region's bitmap
@@ -1146,29 +846,15 @@ __global__ __launch_bounds__(256) void k_ba_final(const uint32_t *__restrict__ n
 }
 
 // launcher ---------------------------------------------------------------------------------
-// EXPERIMENTS (rbx_tune "add_region_grid"): k_ba_region blocks; each walks regions r, r + grid, ...
-static uint32_t g_region_grid = 2048;
+// rbx_tune "add_region_grid": k_ba_region6 blocks; each walks regions r, r + grid, ...
+static std::atomic<uint32_t> g_region_grid{2048};
 void set_add_region_grid(int v) { g_region_grid = (uint32_t)v; }
-// EXPERIMENTS (rbx_tune "add_region_kernel"): 2 (default) 6-byte region pairs + the pipelined
-// k_ba_region6; 1 the r02 8-byte pairs + k_ba_region (A/B only)
-static int g_region_kernel = 2;
-void set_add_region_kernel(int v) { g_region_kernel = v; }
 // rbx_tune "add_rec_lds_limit" (tests): owner records a k_ba_region6 block stages in LDS before it
 // reports a region's owners by direct atomics instead (default and maximum kBa6Main)
-static uint32_t g_rec_limit = kBa6Main;
+static std::atomic<uint32_t> g_rec_limit{kBa6Main};
 void set_add_rec_lds_limit(int v) { g_rec_limit = (uint32_t)v; }
-// EXPERIMENTS (rbx_tune "add_rebucket_prefetch"): 1 = the next tile's loads issued after the
-// placement (default), 0 = at the top of each tile
-static int g_rebucket_prefetch = 1;
-void set_add_rebucket_prefetch(int v) { g_rebucket_prefetch = v; }
-// EXPERIMENTS (rbx_tune "add_stage1_prefetch"): 1 = stage 1 loads the next tile's fixed-length keys
-// into registers after this tile's hash (default), 0 = each tile loads its own
-static int g_stage1_prefetch = 1;
-void set_add_stage1_prefetch(int v) { g_stage1_prefetch = v; }
-// rbx_tune "add_rebucket_lines" (r05): 1 = the whole-line rebucket k_ba_emit2, 0 = k_ba_rebucket, 2 =
-// k_ba_emit2 when the chunk has >= 1024 stage-1 partitions (C2), else k_ba_rebucket (C1: 48)
-static int g_rebucket_lines = 0;
-void set_add_rebucket_lines(int v) { g_rebucket_lines = v; }
+// (r02-r05 A/B switches removed in r06 with the variants they selected: add_region_kernel (8-byte
+// pairs + k_ba_region), add_rebucket_lines (k_ba_emit2), add_rebucket_prefetch 0, add_stage1_prefetch 0.)
 
 template <int KLEN, int KMAX>
 static void ba_chunk(const BaArgs &a, hipStream_t st) {
@@ -1179,51 +865,35 @@ static void ba_chunk(const BaArgs &a, hipStream_t st) {
     const unsigned zgrid = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(na, nb / 4) / 1024 + 1);
     hipLaunchKernelGGL(k_ba_mode, dim3(zgrid), dim3(1024), 0, st, (const uint32_t *)a.f.bm, a.nwords4, a.record_policy,
                        a.mode, a.cnt1, na, a.new_bits, nb);
-    if (g_stage1_prefetch)
-        hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, true>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
-                           dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
-                           a.overflow);
-    else
-        hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, false>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
-                           dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
-                           a.overflow);
+    hipLaunchKernelGGL((k_ba_stage1<KLEN, KMAX, true>), dim3((unsigned)std::min<uint64_t>(ntiles, 4096)),
+                       dim3(kBaS1Threads), 0, st, a.keys, a.base, a.nchunk, a.f, a.s1, a.ncoarse, a.cap1, a.p1, a.cnt1,
+                       a.overflow);
     const uint32_t it1 = (uint32_t)((a.cap1 + kBaRbTile - 1) / kBaRbTile);
-    const dim3 rgrid(std::min<uint32_t>(a.nregions, g_region_grid));
-    unsigned long long *rst = a.stamps ? a.stamps + 8 : nullptr;
-#define BA_REBUCKET(P6, ST, PF)                                                                                          \
-    hipLaunchKernelGGL((k_ba_rebucket<P6, ST, PF>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, \
-                       kBaSub, it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
-#define BA_EMIT2(ST)                                                                                                     \
-    hipLaunchKernelGGL((k_ba_emit2<6, ST>), dim3(nparts), dim3(1024), 0, st, a.p1, a.cnt1, a.cap1, a.ncoarse, kBaSub, a.s3, \
-                       a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
-    const uint32_t nparts = a.ncoarse * kBaSub;
-    const bool lines = g_region_kernel != 1 && (g_rebucket_lines == 1 || (g_rebucket_lines == 2 && nparts >= 1024));
-    if (lines && a.stamps) BA_EMIT2(true);
-    else if (lines) BA_EMIT2(false);
-    else if (g_region_kernel == 1) BA_REBUCKET(false, false, false);
-    else if (a.stamps) BA_REBUCKET(true, true, true);
-    else if (g_rebucket_prefetch) BA_REBUCKET(true, false, true);
-    else BA_REBUCKET(true, false, false);
-#undef BA_REBUCKET
-#undef BA_EMIT2
-    if (g_region_kernel == 1) {
-        if (a.stamps)
-            hipLaunchKernelGGL(k_ba_region<true>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,
-                               a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
-                               a.mode, a.diag, a.stamps);
-        else
-            hipLaunchKernelGGL(k_ba_region<false>, rgrid, dim3(kBaRegionThreads), 0, st, a.p3, a.cnt3, a.cap3, a.nregions,
-                               a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges, a.overflow,
-                               a.mode, a.diag, a.stamps);
-    } else {
+    const dim3 rgrid(std::min<uint32_t>(a.nregions, g_region_grid.load()));
+    // phase stamps (rbx_bench_add_stamps) only in the profiling build
+    const bool stamps = kDiag && a.stamps;
+    unsigned long long *rst = stamps ? a.stamps + 8 : nullptr;
+#define BA_REBUCKET(ST)                                                                                                  \
+    hipLaunchKernelGGL((k_ba_rebucket<true, ST, true>), dim3(2048), dim3(kBaRbThreads), 0, st, a.p1, a.cnt1, a.cap1,      \
+                       a.ncoarse, kBaSub, it1, a.s3, a.f3, a.nregions, a.p3, a.cnt3, a.cap3, a.overflow, rst)
 #define BA_REGION6(ST)                                                                                                    \
-    hipLaunchKernelGGL((k_ba_region6<ST>),    rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3, a.cap3, \
+    hipLaunchKernelGGL((k_ba_region6<ST>), rgrid, dim3(kBaRegionThreads), 0, st, (const uint32_t *)a.p3, a.cnt3, a.cap3,   \
                        a.nregions, a.f.bm, a.nwords4, a.new_bits, a.ctr, a.recs, a.rec_cnt, a.cap_rec, a.nranges,          \
-                       a.overflow, a.mode, g_rec_limit, a.diag, a.stamps)
-        if (a.stamps) BA_REGION6(true);
-        else BA_REGION6(false);
-#undef BA_REGION6
+                       a.overflow, a.mode, g_rec_limit.load(), a.diag, stamps ? a.stamps : nullptr)
+    if constexpr (kDiag) {
+        if (stamps) {
+            BA_REBUCKET(true);
+            BA_REGION6(true);
+        } else {
+            BA_REBUCKET(false);
+            BA_REGION6(false);
+        }
+    } else {
+        BA_REBUCKET(false);
+        BA_REGION6(false);
     }
+#undef BA_REBUCKET
+#undef BA_REGION6
     hipLaunchKernelGGL(k_ba_keys_rec, dim3(std::min<uint32_t>(a.nranges * a.f.k, 2048)), dim3(1024), 0, st, a.recs,
                        a.rec_cnt, a.cap_rec, a.nranges, a.f.k, a.new_bits, a.overflow, a.mode);
     // one thread per 32 keys (a per-thread chain over a smaller grid was the C1 add's third-largest cost);

@@ -19,6 +19,8 @@
 // M/ = /root/reference/redisson/src/main/java/org/redisson/
 #include "bloom_common.h"
 
+#include <atomic>
+
 namespace rbx {
 
 // ---------------------------------------------------------------------------------
@@ -108,8 +110,7 @@ template <int KLEN, int KMAX, int S1>
 __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint32_t *__restrict__ bm,
                                                         ModParams mp, uint32_t k,
                                                         uint8_t *__restrict__ out,
-                                                        unsigned long long *__restrict__ count,
-                                                        unsigned long long *__restrict__ partials) {
+                                                        unsigned long long *__restrict__ count) {
     uint64_t present = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < keys.n; i += stride) {
@@ -119,16 +120,7 @@ __global__ __launch_bounds__(256) void k_bloom_contains(KeysDev keys, const uint
         if (out) out[i] = p;
         present += p;
     }
-    if (partials) block_store_u64(present, partials + blockIdx.x);  // summed by k_add_partials
-    else if (count) block_add_u64(present, count);
-}
-
-// *count += the n per-block partials (one block; one atomic)
-__global__ __launch_bounds__(256) void k_add_partials(const unsigned long long *__restrict__ partials, uint32_t n,
-                                                      unsigned long long *__restrict__ count) {
-    uint64_t v = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) v += partials[i];
-    block_add_u64(v, count);
+    if (count) block_add_u64(present, count);
 }
 
 // tile_seg0[t] = segment of key t*256 (one parallel binary search per 256-key tile)
@@ -657,50 +649,35 @@ __global__ __launch_bounds__(256) void k_digest(const uint8_t *__restrict__ byte
 // ---------------------------------------------------------------------------------
 
 // Early-exit width for contains (rbx_tune("contains_stage1", n)); 0 disables.
-static int g_stage1 = 4;
+static std::atomic<int> g_stage1{4};
 void set_contains_stage1(int v) { g_stage1 = v; }
 int get_contains_stage1() { return g_stage1; }
 
 template <int KLEN, int KMAX, int S1>
 static void launch_contains_s(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
-                              unsigned long long *partials = nullptr) {
-    unsigned long long *pp = count ? partials : nullptr;
-    hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count, pp);
-    if (pp) hipLaunchKernelGGL(k_add_partials, dim3(1), dim3(256), 0, st, pp, grid, count);
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    hipLaunchKernelGGL((k_bloom_contains<KLEN, KMAX, S1>), dim3(grid), dim3(256), 0, st, keys, bm, mp, k, out, count);
 }
 
-static unsigned g_qgrid = 2048;  // slot kernel grid (grid-stride over 64*Q-key ranges)
-static int g_qshape = 22;        // slot kernel: P * 10 + Q (slots per lane, queue keys per lane)
-void set_contains_qshape(int v) { g_qshape = v; }
+// slot kernel grid (grid-stride over 64*Q-key ranges), rbx_tune "contains_qgrid".  Its shape is P = 2
+// slots and Q = 2 queued keys per lane (r02-r05 also compiled 24/32/34/42/44 for A/Bs: none faster,
+// removed in r06; profiles/r03/r03u_c5sweep_qshape_qgrid.jsonl).
+static std::atomic<unsigned> g_qgrid{2048};
 void set_contains_qgrid(int v) { g_qgrid = (unsigned)v; }
 
 template <int KLEN, bool MULTI>
 static void launch_contains_q(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off, uint32_t nseg,
                               const uint32_t *tile_seg0, const FilterDesc &single, uint8_t *out,
                               unsigned long long *counts, hipStream_t st, unsigned grid) {
-    const dim3 g(std::min(grid, g_qgrid)), b(256);
-#define RBX_Q(P, Q) hipLaunchKernelGGL((k_bloom_contains_q<KLEN, MULTI, P, Q>), g, b, 0, st, keys, filt, seg_off, nseg, \
-                                       tile_seg0, single, out, counts)
-    if constexpr (KLEN == 16) {
-        switch (g_qshape) {
-        case 24: RBX_Q(2, 4); return;
-        case 42: RBX_Q(4, 2); return;
-        case 32: RBX_Q(3, 2); return;
-        case 34: RBX_Q(3, 4); return;
-        case 44: RBX_Q(4, 4); return;
-        default: break;
-        }
-    }
-    RBX_Q(2, 2);
-#undef RBX_Q
+    hipLaunchKernelGGL((k_bloom_contains_q<KLEN, MULTI, 2, 2>), dim3(std::min(grid, g_qgrid.load())), dim3(256), 0, st,
+                       keys, filt, seg_off, nseg, tile_seg0, single, out, counts);
 }
 
 template <int KLEN, int KMAX>
 static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
-                               unsigned long long *partials) {
-    if (g_stage1 == 5 && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
+                               uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    const int stage1 = g_stage1.load();  // read once per call
+    if (stage1 == 5 && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
         FilterDesc f{};
         f.bm = const_cast<uint32_t *>(bm);
         f.mp = mp;
@@ -708,33 +685,31 @@ static void launch_contains_km(const KeysDev &keys, const uint32_t *bm, const Mo
         launch_contains_q<KLEN, false>(keys, nullptr, nullptr, 0u, nullptr, f, out, count, st, grid);
         return;
     }
-    switch (g_stage1) {
-    case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    case 3: launch_contains_s<KLEN, KMAX, 3>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    case 4: launch_contains_s<KLEN, KMAX, 4>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    default: launch_contains_s<KLEN, KMAX, 1>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    switch (stage1) {
+    case 0: launch_contains_s<KLEN, KMAX, 0>(keys, bm, mp, k, out, count, st, grid); break;
+    case 2: launch_contains_s<KLEN, KMAX, 2>(keys, bm, mp, k, out, count, st, grid); break;
+    case 3: launch_contains_s<KLEN, KMAX, 3>(keys, bm, mp, k, out, count, st, grid); break;
+    case 4: launch_contains_s<KLEN, KMAX, 4>(keys, bm, mp, k, out, count, st, grid); break;
+    default: launch_contains_s<KLEN, KMAX, 1>(keys, bm, mp, k, out, count, st, grid); break;
     }
 }
 
 template <int KLEN>
 static void launch_contains_k(const KeysDev &keys, const uint32_t *bm, const ModParams &mp, uint32_t k,
-                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid,
-                              unsigned long long *partials) {
-    if (k <= 8) launch_contains_km<KLEN, 8>(keys, bm, mp, k, out, count, st, grid, partials);
-    else if (k <= 16) launch_contains_km<KLEN, 16>(keys, bm, mp, k, out, count, st, grid, partials);
-    else launch_contains_s<KLEN, 0, 0>(keys, bm, mp, k, out, count, st, grid, partials);
+                              uint8_t *out, unsigned long long *count, hipStream_t st, unsigned grid) {
+    if (k <= 8) launch_contains_km<KLEN, 8>(keys, bm, mp, k, out, count, st, grid);
+    else if (k <= 16) launch_contains_km<KLEN, 16>(keys, bm, mp, k, out, count, st, grid);
+    else launch_contains_s<KLEN, 0, 0>(keys, bm, mp, k, out, count, st, grid);
 }
 
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
-                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st,
-                           unsigned long long *partials) {
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st) {
     const unsigned grid = grid_for(keys.n, kMaxGrid);
     switch (klen_fast) {
-    case 16: launch_contains_k<16>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    case 32: launch_contains_k<32>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    case 64: launch_contains_k<64>(keys, bm, mp, k, out, count, st, grid, partials); break;
-    default: launch_contains_k<0>(keys, bm, mp, k, out, count, st, grid, partials); break;
+    case 16: launch_contains_k<16>(keys, bm, mp, k, out, count, st, grid); break;
+    case 32: launch_contains_k<32>(keys, bm, mp, k, out, count, st, grid); break;
+    case 64: launch_contains_k<64>(keys, bm, mp, k, out, count, st, grid); break;
+    default: launch_contains_k<0>(keys, bm, mp, k, out, count, st, grid); break;
     }
 }
 
@@ -742,8 +717,9 @@ template <int KLEN>
 static void launch_contains_multi_k(const KeysDev &keys, const FilterDesc *filt, const uint64_t *seg_off,
                                     uint32_t nseg, const uint32_t *tile_seg0, uint32_t kmax, uint8_t *out,
                                     unsigned long long *counts, hipStream_t st, unsigned grid, bool slots) {
-    const bool dbl = g_stage1 == 4;
-    if ((slots || g_stage1 == 5) && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
+    const int stage1 = g_stage1.load();  // read once per call
+    const bool dbl = stage1 == 4;
+    if ((slots || stage1 == 5) && keys.n < (1ULL << 32)) {  // slot kernel: u32 key indexes
         launch_contains_q<KLEN, true>(keys, filt, seg_off, nseg, tile_seg0, FilterDesc{}, out, counts, st, grid);
         return;
     }

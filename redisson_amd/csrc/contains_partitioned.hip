@@ -83,6 +83,7 @@ __global__ __launch_bounds__(NT) void k_bk_stage1(KeysDev keys, uint64_t base, u
                                                    unsigned long long *__restrict__ pairs1, uint32_t *__restrict__ cnt1,
                                                    unsigned long long *__restrict__ alive,
                                                    unsigned long long *__restrict__ miss, uint32_t flags) {
+    if (!kDiag) flags = 0;  // wrong-answer diagnostics exist in the profiling build only (rbx_kernels.h)
     constexpr int TILE = NT * PER;
     // dynamic LDS (bk_stage1_lds): image of a tile's pairs with each bucket's carried pairs in
     // front of its new ones, the bucket id of every image slot, the carries, the counters
@@ -242,6 +243,7 @@ __global__ __launch_bounds__(NT) void k_bk_emit2(const unsigned long long *__res
                                                   uint32_t *__restrict__ cnt2,
                                                   const uint32_t *__restrict__ bm, unsigned long long *__restrict__ miss,
                                                   uint32_t flags, unsigned long long *__restrict__ stamps) {
+    if (!kDiag) flags = 0;  // wrong-answer diagnostics exist in the profiling build only (rbx_kernels.h)
     PhaseStamps<STAMP, 4> ps;
     ps.start();
     // PER u32x4 (two pairs each) per thread
@@ -395,6 +397,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                    unsigned long long *__restrict__ miss, uint32_t *__restrict__ mrec,
                                                    uint32_t *__restrict__ mcnt, uint64_t capm, uint32_t nmranges,
                                                    uint32_t flags, unsigned long long *__restrict__ stamps) {
+    if (!kDiag) flags = 0;  // wrong-answer diagnostics exist in the profiling build only (rbx_kernels.h)
     PhaseStamps<STAMP, 4> ps;
     ps.start();
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[kBkRegionWords];
@@ -592,26 +595,15 @@ static void bk_emit2(const PcArgs &a, hipStream_t st) {
                            nullptr);
 }
 
-// EXPERIMENTS (rbx_tune "contains_emit2_nt"): emit2 shape.  1536 (default): 1024 threads, 12K-pair
-// tiles, 131 KiB of LDS, one block per CU; 1024: 8K-pair tiles (96 KiB; C2 4.84 -> 4.74 ms with 12K,
-// profiles/r02/r02u_abt_c2_emit2_tiles.jsonl); 1792: 14K-pair tiles; 512: 512 threads, 4K-pair tiles
-// (67 KiB, two blocks per CU).
-static int g_emit2_nt = 1536;
-void set_contains_emit2_nt(int v) { g_emit2_nt = v; }
-// EXPERIMENTS (rbx_tune "contains_stage1_per"): keys per stage-1 thread for k <= 8 (2 = default:
-// 1024-key tiles, ~75 KiB of LDS, two blocks per CU; 1: 512-key tiles, three blocks per CU)
-static int g_stage1_per = 2;
-void set_contains_stage1_per(int v) { g_stage1_per = v; }
-
+// Shapes: stage 1 at 512 threads with bk_per<KMAX>() keys per thread (1024-key tiles at k <= 8, ~75 KiB
+// of LDS, two blocks per CU); emit2 at 1024 threads with 12K-pair tiles (131 KiB, one block per CU; C2
+// 4.84 -> 4.74 ms against 8K, profiles/r02/r02u_abt_c2_emit2_tiles.jsonl).  (The A/B shapes behind
+// rbx_tune "contains_emit2_nt" / "contains_stage1_per" were removed in r06.)
 template <int KLEN, int KMAX>
 static void bk_chunk(const PcArgs &a, hipStream_t st) {
-    if (KMAX <= 8 && g_stage1_per == 1) bk_stage1<KLEN, KMAX, 512, 1>(a, st);
-    else bk_stage1<KLEN, KMAX, 512, bk_per<KMAX>()>(a, st);
-    if (g_emit2_nt == 512) bk_emit2<512, 4>(a, st);
-    else if (g_emit2_nt == 1024) bk_emit2<1024, 4>(a, st);  // 8K-pair tiles
-    else if (g_emit2_nt == 1792) bk_emit2<1024, 7>(a, st);  // 14K-pair tiles
-    else bk_emit2<1024, 6>(a, st);                          // 12K-pair tiles (default)
-    if (a.stamps)
+    bk_stage1<KLEN, KMAX, 512, bk_per<KMAX>()>(a, st);
+    bk_emit2<1024, 6>(a, st);
+    if (kDiag && a.stamps)
         hipLaunchKernelGGL((k_bk_probe<true>), dim3(std::min<uint32_t>(a.nregions, 2048)), dim3(1024), 0, st, a.p2lo,
                            a.p2hi, a.cnt2, a.cap2, a.nregions, a.bm, a.nwords4, a.miss, a.mrec, a.mcnt, a.capm, a.nmranges,
                            a.flags, a.stamps + 8);

@@ -186,13 +186,12 @@ struct rbx_ctx {
     DevBuf pc_bits, pc_cnt, pc_pairs1, pc_pairs2, pc_mrec;  // partitioned contains
     DevBuf pa_p1, pa_p2, pa_cnt, pa_bits, pa_ctr, pa_recs;  // partitioned add
     DevBuf pa_stamps;  // add_partition_diag & 64: region-pass phase times (rbx_bench_add_stamps)
-    DevBuf st_adds, st_prefilter;                   // ordered stream: add list, prefilter + counter
-    DevBuf st_occ;               // ordered stream (r04): occupancy bitmap of st_t8's slots
-    DevBuf st_t8, st_flag;       // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks), owner flags
+    DevBuf st_adds, st_nadds;    // ordered stream: add list, one add counter per chunk
+    DevBuf st_t8;                // ordered stream (r04): 8-byte first-setter table (EMPTY between chunks)
     DevBuf st_fslot;             // ordered stream (r05): per add, the slot of its first zero bit's claim
     DevBuf madd_c;               // multi-tenant add (r05): conflict table C + its MaddxState (+ the `big` flag)
     uint64_t madd_maxseg_hint = ~0ULL;  // set by the host-arena add_multi: its largest segment (keys)
-    uint64_t st_t8_entries = 0, st_flag_bytes = 0;  // initialized sizes of the two
+    uint64_t st_t8_entries = 0;  // initialized size of st_t8
     uint64_t st_geom[4] = {0, 0, 0, 0};             // last stream call: bb, fbits, pb, chunk
     DevBuf fid_table;            // bitmap words per table id (fid) of the filters of filt_table
     uint32_t filt_nfids = 0;     // distinct table ids of filt_table
@@ -235,12 +234,12 @@ struct rbx_ctx {
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf slot_bytes[2], slot_offs[2];
-    DevBuf partials;  // per-block counts of the direct contains kernel (contains_partials)
     uint64_t staging_bytes = 64ull << 20;
     // small host batches (bloom_host_small): a pinned copy of the keys, uploaded on `stream` with the
     // zeroed count word in one transfer; the count and flags come back into it
     void *pin_small = nullptr;
     size_t pin_small_cap = 0;
+    uint64_t pin_small_limit = 0;  // the host_small_bytes the block was laid out for (its tail offset)
     unsigned long long *pin_word = nullptr;  // pinned readback words (counts, the partitioned add's overflow flag)
 
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
@@ -586,9 +585,9 @@ static int run_add_table(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_fi
 // grows with the bitmap (0.7 ms at 512 MiB) while the table path's cost grows with the batch
 // (0.7 us per 1K keys): crossovers ~150K keys at 12-32 MiB, ~1M at 512 MiB
 // (tools/microbench.py addsweep, profiles/r02/r02h_addsweep_table_vs_partitioned.jsonl).
-static int g_add_partition_mode = 2;
-static int g_add_partition_diag = 0;
-static int g_add_record_policy = 2;
+static std::atomic<int> g_add_partition_mode{2};
+static std::atomic<int> g_add_partition_diag{0};
+static std::atomic<int> g_add_record_policy{2};
 
 static bool use_add_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 1 || k > 16 || size > (1ULL << 32) || size < (1ULL << 15)) return false;
@@ -713,12 +712,8 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
 // 1 whenever k in [2, 16], 2 (default) when the bitmap is >= 256 MiB and the batch >= 4M keys.
 // Below 256 MiB the direct kernel measured faster (its early exit costs ~1 gather per absent
 // key, and smaller bitmaps gather partly from L2/MALL); DESIGN.md §3.6 has the size sweep.
-static int g_partition_mode = 2;
-static int g_partition_flags = 0;
-
-// rbx_tune("contains_partials"): 1 = the direct contains kernel stores per-block counts that one small kernel
-// adds up, 0 = one atomic per block into the count (they serialise at the kernel's end)
-static int g_contains_partials = 0;
+static std::atomic<int> g_partition_mode{2};
+static std::atomic<int> g_partition_flags{0};
 
 static bool use_partitioned(uint64_t size, uint32_t k, uint64_t n) {
     if (k < 2 || k > 16 || size > (1ULL << 32)) return false;
@@ -809,12 +804,7 @@ static int run_contains_partitioned(rbx_ctx *c, const KeysDev &keys, const Filte
 static int run_contains(rbx_ctx *c, const KeysDev &keys, const FilterDesc &f, uint8_t *d_out,
                         unsigned long long *d_count, hipStream_t st) {
     if (use_partitioned(f.mp.size, f.k, keys.n)) return run_contains_partitioned(c, keys, f, d_out, d_count, st);
-    unsigned long long *partials = nullptr;
-    if (g_contains_partials && d_count) {  // per-block counts + one summing launch (see launch_bloom_contains)
-        RBX_TRY(c->partials.reserve(kMaxGrid * 8));
-        partials = c->partials.as<unsigned long long>();
-    }
-    launch_bloom_contains(keys, fast_len(keys), f.bm, f.mp, f.k, d_out, d_count, st, partials);
+    launch_bloom_contains(keys, fast_len(keys), f.bm, f.mp, f.k, d_out, d_count, st);
     HIP_TRY(hipGetLastError());
     return RBX_OK;
 }
@@ -905,15 +895,15 @@ int rbx_shutdown(rbx_ctx *c) {
         c->hll_chunks.clear();
         c->hll_free.clear();
         c->hll_dirty.clear();
-        c->st_t8_entries = c->st_flag_bytes = 0;
+        c->st_t8_entries = 0;
         c->slab.reset();  // bitmaps still held by open handles keep their slab alive
         for (DevBuf *b : {&c->table, &c->zmask, &c->keys_bytes, &c->keys_offs, &c->out_bytes, &c->seg_offs,
                           &c->counters, &c->filt_table, &c->probe_table, &c->ptrs, &c->histo, &c->misc, &c->tile_segs,
                           &c->hll_tiles, &c->pc_bits, &c->pc_cnt, &c->pc_pairs1, &c->pc_pairs2, &c->pc_mrec,
                           &c->pa_p1, &c->pa_p2, &c->pa_cnt, &c->pa_bits, &c->pa_ctr, &c->pa_recs, &c->st_adds,
-                          &c->st_prefilter, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
-                          &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->st_flag, &c->fid_table,
-                          &c->hll_zero_ptrs, &c->wide_table, &c->st_occ, &c->st_fslot, &c->madd_c, &c->partials}) {
+                          &c->st_nadds, &c->zero_bm, &c->hll_pack, &c->slot_bytes[0], &c->slot_bytes[1],
+                          &c->slot_offs[0], &c->slot_offs[1], &c->st_t8, &c->fid_table,
+                          &c->hll_zero_ptrs, &c->wide_table, &c->st_fslot, &c->madd_c}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -928,6 +918,7 @@ int rbx_shutdown(rbx_ctx *c) {
         if (c->pin_small) (void)hipHostFree(c->pin_small);
         c->pin_small = nullptr;
         c->pin_small_cap = 0;
+        c->pin_small_limit = 0;
         if (c->pin_word) (void)hipHostFree(c->pin_word);
         c->pin_word = nullptr;
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -1076,7 +1067,7 @@ extern "C" {
 // RBX_E_REDIS (RedisException) -- an add has set every in-range bit.  Without such an index the
 // replies are the in-order ones.  Chunks run in key order (each sees the previous chunks' bits).
 // rbx_tune("wide_subchunk", n): keys per sub-chunk cap (0 = default 2^29 / k; tests split small batches)
-static uint64_t g_wide_subchunk = 0;
+static std::atomic<uint64_t> g_wide_subchunk{0};
 static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t k, Bitmap *bm, uint8_t *out_flags,
                          uint64_t *out_count, bool is_add) {
     RBX_TRY(c->counters.reserve(64));
@@ -1135,32 +1126,44 @@ static int bloom_wide_op(rbx_ctx *c, const rbx_keys *keys, uint64_t m, uint32_t 
 // into the same pinned block with one sync.  (The pipelined path costs a fill, a sync, a copy-stream
 // upload from pageable memory with two event hops, and a second sync: ~62 us for one key on the r05
 // boxes, tools/microbench.py smallbatch.)
-static int g_small_host = 1;  // rbx_tune("host_small_batches"): 0 = every host batch on the pipelined path
-static uint64_t g_small_bytes = 4 << 20;  // rbx_tune("host_small_bytes"): the byte limit (keys <= limit / 4)
+static std::atomic<int> g_small_host{1};  // rbx_tune("host_small_batches"): 0 = every host batch on the pipelined path
+static std::atomic<uint64_t> g_small_bytes{4 << 20};  // rbx_tune("host_small_bytes"): the byte limit (keys <= limit / 4)
 static constexpr uint64_t kSmallHead = 64 << 10;  // zeroed result area ahead of the keys (counts, changed words)
-static size_t small_pin_bytes() { return kSmallHead + g_small_bytes + g_small_bytes / 4 + 64; }  // head | keys | tail
+static size_t small_pin_bytes(uint64_t limit) { return kSmallHead + limit + limit / 4 + 64; }  // head | keys | tail
 
-// the pinned block of the one-transfer path, (re)allocated for the current limit; false (the caller takes
-// the pipelined path) when pinned memory cannot be had
-static bool small_pinned(rbx_ctx *c) {
-    const size_t pin = small_pin_bytes();
-    if (c->pin_small_cap >= pin) return true;
+// the pinned block of the one-transfer path, laid out for host_small_bytes = limit (or a larger limit it
+// already had); false (the caller takes the pipelined path) when pinned memory cannot be had
+static bool small_pinned(rbx_ctx *c, uint64_t limit) {
+    if (c->pin_small && c->pin_small_limit >= limit) return true;
     if (c->pin_small) (void)hipHostFree(c->pin_small);
     c->pin_small = nullptr;
     c->pin_small_cap = 0;
+    c->pin_small_limit = 0;
+    const size_t pin = small_pin_bytes(limit);
     if (hipHostMalloc(&c->pin_small, pin, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         c->pin_small = nullptr;
         return false;
     }
     c->pin_small_cap = pin;
+    c->pin_small_limit = limit;
     return true;
 }
 
+// the process-wide limit is read ONCE here (rbx_tune may change it on another thread);
+// the staging below uses the block's own layout (c->pin_small_limit >= the limit checked here)
 static bool bloom_small_fits(rbx_ctx *c, const rbx_keys *k) {
-    if (!g_small_host || k->n == 0 || k->n > g_small_bytes / 4) return false;
+    const uint64_t limit = g_small_bytes;
+    if (!g_small_host || k->n == 0 || k->n > limit / 4) return false;
     const uint64_t nb = k->offsets ? k->offsets[k->n] - k->offsets[0] : k->n * k->stride;
-    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= g_small_bytes && small_pinned(c);
+    return nb + (k->offsets ? (k->n + 1) * 8 + 8 : 0) <= limit && small_pinned(c, limit);
+}
+
+// an error after small_stage queued the upload: the copy and any launches may still be reading the pinned
+// block and slot 0, which the next small call overwrites -- drain the stream first
+static int small_fail(rbx_ctx *c, int rc) {
+    (void)hipStreamSynchronize(c->stream);
+    return rc;
 }
 
 // One-transfer staging of a small host arena (bloom_small_fits): pinned [0, head) zeroed, the key bytes
@@ -1173,7 +1176,7 @@ struct SmallStage {
 };
 static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallStage *s, const void *head_src = nullptr,
                        uint64_t head_src_at = 0, uint64_t head_src_len = 0) {
-    const size_t pin = small_pin_bytes();  // allocated by bloom_small_fits (small_pinned)
+    const size_t pin = c->pin_small_cap;  // allocated by bloom_small_fits (small_pinned)
     head = (std::max<uint64_t>(head, 8) + 63) / 64 * 64;  // <= kSmallHead (callers bound it)
     uint8_t *hp = (uint8_t *)c->pin_small;
     const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
@@ -1189,7 +1192,7 @@ static int small_stage(rbx_ctx *c, const rbx_keys *keys, uint64_t head, SmallSta
     HIP_TRY(hipMemcpyAsync(dp, hp, end, hipMemcpyHostToDevice, c->stream));
     s->hp = hp;
     s->dp = dp;
-    s->tail_h = hp + kSmallHead + g_small_bytes;
+    s->tail_h = hp + kSmallHead + c->pin_small_limit;
     s->dk = KeysDev{dp + head, off_at ? (const uint64_t *)(dp + off_at) : nullptr, keys->stride, n, off_at ? b0 : 0};
     return RBX_OK;
 }
@@ -1208,7 +1211,7 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
     const int rc = is_add ? run_add(c, s.dk, nullptr, nullptr, 0, f, k, d_out, d_count, nullptr, c->stream)
                           : run_contains(c, s.dk, f, d_out, d_count, c->stream);
     (void)hipEventRecord(c->ev_done[0], c->stream);  // slot 0 read by what was queued, whatever rc
-    RBX_TRY(rc);
+    if (rc != RBX_OK) return small_fail(c, rc);
     // the readback lands in the pinned block: its upload precedes it on the stream
     HIP_TRY(hipMemcpyAsync(s.hp, s.dp, 8, hipMemcpyDeviceToHost, c->stream));
     if (out_flags) HIP_TRY(hipMemcpyAsync(s.tail_h, d_out, n, hipMemcpyDeviceToHost, c->stream));
@@ -1584,7 +1587,7 @@ int rbx_bloom_add_dev(rbx_ctx *c, rbx_bloom *b, const rbx_keys *d_keys, uint8_t 
 // the distinct bitmaps of a call exceed this many bytes (past the caches, the request count
 // binds); below it the staged kernel (fewer instructions per key) is faster.  rbx_tune
 // "contains_multi_slots": 0 never, 1 always, 2 by this threshold (default).
-static int g_multi_slots = 2;
+static std::atomic<int> g_multi_slots{2};
 constexpr uint64_t kSlotsMinBytes = 64ULL << 20;
 
 // create: a missing bitmap is created (add, stream); otherwise (contains) it reads as all zero
@@ -1714,34 +1717,37 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
 
 // rbx_tune("stream_chunk", n) caps a chunk of the ordered stream and of the 8-byte multi-tenant add at
 // n commands (tests: many chunks on small batches).
-static uint64_t g_stream_chunk = 0;
+static std::atomic<uint64_t> g_stream_chunk{0};
 // rbx_tune("add_multi_table8"): multi-tenant adds whenever (filter id, bit) fits 41 bits and k <= 32:
-// 2 (default) optimistic SETBITs with conflict repair (k_maddx_*, r05), 1 the 8-byte first-setter table
-// with the walk commit (k_madd_*, r05), 0 the r03 16-byte table path
-static int g_add_multi_t8 = 2;
+// 2 (default) optimistic SETBITs with conflict repair (k_maddx_*, r05), 0 the r03 16-byte table path
+// (the fallback past 41 bits or k > 32; tests).  (1, the 8-byte first-setter table with the walk
+// commit, measured 74.5 vs 53.3 ms at C3 and was removed in r06.)
+static std::atomic<int> g_add_multi_t8{2};
 // rbx_tune("add_multi_conflict_log2"): entries of the conflict table C, log2 (default 17: 1 MiB, L2-
 // resident; tests use small ones to run the overflow path)
-static uint32_t g_maddx_lgc = 17;
+static std::atomic<uint32_t> g_maddx_lgc{17};
 // rbx_tune("add_multi_segment"): 1 (default) a batch whose filters are all distinct runs its segments of
 // <= add_multi_segmax keys one workgroup each (k_madd_seg: LDS first setters, plain word stores, no
 // memory-side atomics), longer segments on the chunked path; 0 everything on the chunked path
-static int g_madd_seg = 1;
-static uint64_t g_madd_segmax = 16384;
-// rbx_tune("add_multi_seg_lgs"): log2 of the per-segment kernel's LDS table slots, 11 or 12 (a tile never
-// holds more than 2048 zero bits: tile x kmax <= 2048, so 2^11 slots never fill)
-static uint32_t g_madd_seg_lgs = 12;
+static std::atomic<int> g_madd_seg{1};
+static std::atomic<uint64_t> g_madd_segmax{16384};
+// rbx_tune("add_multi_seg_grid"): the per-segment kernel's workgroups, grid-stride over the segments
+// (8192: C3 add 28.5 ms; 4096 28.9, 2048 29.9, 1024 31.1, 512 32.7; profiles/r06/r06d_*)
+static std::atomic<uint32_t> g_madd_seg_grid{8192};
 
-// Multi-tenant add on the 8-byte table: chunks of <= min(2^pb - 1, 2^27 / k) keys, each probe ->
-// final -> walk, in key order (a chunk's bits are set before the next probes).  The table and its
-// EMPTY state are shared with the ordered stream (st_t8 / st_t8_entries).
+// Multi-tenant add by optimistic SETBITs with conflict repair (k_maddx_*): chunks of <= min(2^pb - 1,
+// 2^27 / k) keys in key order (a chunk's bits are set before the next gathers).  The 8-byte table (an
+// overflowed chunk's first setters) and its EMPTY state are shared with the ordered stream (st_t8 /
+// st_t8_entries).
 static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg_off, uint32_t nseg,
                           uint32_t kmax, uint32_t bb, uint32_t pb, uint8_t *d_out_new,
-                          unsigned long long *d_seg_counts, hipStream_t st, const uint32_t *big = nullptr,
-                          uint64_t segmax = 0) {
+                          unsigned long long *d_seg_counts, hipStream_t st, uint64_t lgc,
+                          const uint32_t *big = nullptr, uint64_t segmax = 0) {
     const uint64_t k = std::max<uint32_t>(kmax, 1);
     const uint64_t cap = std::min<uint64_t>((1ULL << std::min<uint32_t>(pb, 40)) - 1, (1ULL << 27) / k);
     uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(keys.n, cap));
-    if (g_stream_chunk) chunk = std::min<uint64_t>(chunk, g_stream_chunk);
+    const uint64_t chunk_cap = g_stream_chunk;  // the knob, once per call
+    if (chunk_cap) chunk = std::min<uint64_t>(chunk, chunk_cap);
     const uint32_t lgmax = t8_log2((uint32_t)chunk, (uint32_t)k);
     const uint64_t entries = 1ULL << lgmax;
     if (c->st_t8_entries < entries) {
@@ -1751,9 +1757,7 @@ static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg
         c->st_t8_entries = entries;
     }
     RBX_TRY(c->zmask.reserve(chunk * 4));
-    RBX_TRY(c->st_fslot.reserve(chunk * 4));
-    const bool optimistic = g_add_multi_t8 == 2;
-    if (optimistic) RBX_TRY(c->madd_c.reserve((8ULL << g_maddx_lgc) + 64));
+    RBX_TRY(c->madd_c.reserve((8ULL << lgc) + 64));
     struct ResetOnError {  // see rbx_bloom_stream_dev
         rbx_ctx *c;
         bool ok = false;
@@ -1778,16 +1782,13 @@ static int run_add_multi8(rbx_ctx *c, const KeysDev &keys, const uint64_t *d_seg
         a.pb = pb;
         a.fid_bm = c->fid_table.as<uint32_t *>();
         a.zmask = c->zmask.as<uint32_t>();
-        a.fslot = c->st_fslot.as<uint32_t>();
         a.out_new = d_out_new;
         a.seg_counts = d_seg_counts;
-        if (optimistic) {
-            a.c8 = c->madd_c.as<unsigned long long>();
-            a.lgC = g_maddx_lgc;
-            a.cst = (MaddxState *)(a.c8 + (1ULL << g_maddx_lgc));
-            a.big = big;
-            a.segmax = segmax;
-        }
+        a.c8 = c->madd_c.as<unsigned long long>();
+        a.lgC = (uint32_t)lgc;
+        a.cst = (MaddxState *)(a.c8 + (1ULL << lgc));
+        a.big = big;
+        a.segmax = segmax;
         launch_madd8_chunk(a, fl, st);
         HIP_TRY(hipGetLastError());
     }
@@ -1813,11 +1814,14 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     uint32_t bb = 1, fbits = 0;
     while ((1ULL << bb) < c->filt_maxbits) ++bb;
     while ((1ULL << fbits) < c->filt_nfids) ++fbits;
-    if (g_add_multi_t8 == 2 && g_madd_seg && kmax <= 16 && c->filt_nfids == nseg && bb + fbits <= 41) {
+    // the knobs, once per call (rbx_tune may run on another thread)
+    const int mode = g_add_multi_t8;
+    const uint64_t lgc = g_maddx_lgc, segmax = g_madd_segmax;
+    if (mode == 2 && g_madd_seg && kmax <= 16 && c->filt_nfids == nseg && bb + fbits <= 41) {
         // every filter in one segment only: k_madd_seg, one workgroup per segment; the chunked path
-        // then handles only segments past segmax (and returns at once when there are none)
-        RBX_TRY(c->madd_c.reserve((8ULL << g_maddx_lgc) + 64));
-        uint32_t *big = (uint32_t *)(c->madd_c.as<unsigned long long>() + (1ULL << g_maddx_lgc)) + 4;
+        // then handles only segments past segmax
+        RBX_TRY(c->madd_c.reserve((8ULL << lgc) + 64));
+        uint32_t *big = (uint32_t *)(c->madd_c.as<unsigned long long>() + (1ULL << lgc)) + 4;
         HIP_TRY(hipMemsetAsync(big, 0, 4, st));
         MaddSegArgs a{};
         a.keys = k;
@@ -1825,47 +1829,35 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
         a.seg_off = d_seg_offsets;
         a.nseg = nseg;
         a.kmax = kmax;
-        a.lgs = g_madd_seg_lgs;  // 2^lgs slots per table, 16 B each (12: 64 KiB of LDS, two workgroups per CU)
-        a.tile = std::max<uint32_t>(64, std::min<uint32_t>(256, (2048 / std::max<uint32_t>(kmax, 1)) & ~63u));
-        a.segmax = g_madd_segmax;
+        a.grid = g_madd_seg_grid;
+        a.segmax = segmax;
         a.out_new = d_out_new;
         a.seg_counts = d_counts;
         a.big = big;
         launch_madd_seg(a, fast_len(k), st);
         HIP_TRY(hipGetLastError());
-        if (c->madd_maxseg_hint <= g_madd_segmax) return RBX_OK;  // host-known: no long segment
-        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, big,
-                              g_madd_segmax);
+        if (c->madd_maxseg_hint <= segmax || d_keys->n <= segmax) return RBX_OK;  // no long segment
+        // device offsets: read the flag (one sync) rather than launch the chunked path's kernels for
+        // nothing -- 60 empty launches per C3 call in r05
+        HIP_TRY(hipMemcpyAsync(c->pin_word, big, 4, hipMemcpyDeviceToHost, st));  // pinned: no staging copy
+        HIP_TRY(hipStreamSynchronize(st));
+        uint32_t has_big;
+        memcpy(&has_big, c->pin_word, 4);
+        if (!has_big) return RBX_OK;
+        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, lgc, big,
+                              segmax);
     }
-    if (g_add_multi_t8 && kmax <= 32 && bb + fbits <= 41)
-        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st);
+    if (mode && kmax <= 32 && bb + fbits <= 41)
+        return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, lgc);
     FilterDesc dummy{};
     return run_add(c, k, c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, dummy, kmax, d_out_new, nullptr,
                    d_counts, st);
 }
 
 // Ordered mixed stream (C5): see rbx.h.  Chunks of <= 2^26 pairs run probe -> contains -> commit.
-// rbx_tune("stream_prefilter"): pbits in [16, 27] = the adds also set a 2^pbits-bit prefilter that a
-// contains reads before it looks a clear bit up in the first-setter table; 0 (default since r04) =
-// the table alone.  With the 8-byte table (64 MiB for a C5 chunk) a lookup costs less than the
-// prefilter's memory-side atomicOr per zero bit: C5 with new (tenant, key) pairs every step 17.0 /
-// 17.1 ms per 1e8 commands vs 17.8 / 17.9 at 2^23 bits, 17.2 / 17.3 at 2^25, 18.4 at 2^22
-// (profiles/r04/r04g_c5_fresh_prefilter.jsonl).  A replayed stream (adds that find no zero bit) is
-// the one case a prefilter pays: 10.2 ms at 2^23 vs 10.8 without.
-static int g_stream_prefilter = 0;
-// rbx_tune("stream_occupancy"): 1 = without a prefilter, a clear bit is looked up in the 8-byte
-// table only when its home slot is occupied (a bitmap of the table's slots, streamed from the table
-// after the probe: k_stream_occ, no atomics); 0 (default) = every clear bit looked up.  Measured
-// slower on the fresh C5 stream: 17.62 / 17.67 / 17.64 vs 17.29 / 17.20 ms per 1e8 commands
-// (profiles/r04/r04o_c5_occupancy_rejected.jsonl): the 64 MiB table's lookups cost less than the
-// extra pass and the bitmap's L2 footprint.
-static int g_stream_occ = 0;
 // rbx_tune("stream_table8"): 1 (default) the 8-byte first-setter table + walk commit (r04) when
-// (fid, bit) fits 41 bits, 0 the r03 16-byte epoch-tagged table
-static int g_stream_table8 = 1;
-// rbx_tune("stream_table_scale"): 1, 2 or 4 -- the 8-byte table holds 2^t8_log2(adds x k x scale)
-// entries (scale 1: load <= 8/9 if every bit of every add were 0)
-static int g_stream_table_scale = 1;
+// (fid, bit) fits 41 bits, 0 the r03 16-byte epoch-tagged table (the fallback past 41 bits; tests)
+static std::atomic<int> g_stream_table8{1};
 int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilters, const uint32_t *d_key_filter,
                          const uint8_t *d_key_op, const rbx_keys *d_keys, uint8_t *d_out,
                          unsigned long long *d_counts, void *stream) {
@@ -1906,37 +1898,28 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
     RBX_TRY(c->zmask.reserve(chunk * 4));
     RBX_TRY(c->st_adds.reserve(chunk * 4));
     if (t8) RBX_TRY(c->st_fslot.reserve(chunk * 4));
-    const uint32_t pbits = g_stream_prefilter ? (uint32_t)g_stream_prefilter : 20u;
-    const uint64_t kPrefilterWords = 1ULL << (pbits - 5);
-    // prefilter words, then one add counter per chunk (zeroed once per call: one fill, not one per chunk)
+    // one add counter per chunk (zeroed once per call: one fill, not one per chunk)
     const uint64_t nchunks = (keys.n + chunk - 1) / chunk;
-    RBX_TRY(c->st_prefilter.reserve((kPrefilterWords + 64 + nchunks) * 4));
-    HIP_TRY(hipMemsetAsync(c->st_prefilter.as<uint32_t>() + kPrefilterWords, 0, nchunks * 4, st));
+    RBX_TRY(c->st_nadds.reserve(nchunks * 4));
+    HIP_TRY(hipMemsetAsync(c->st_nadds.p, 0, nchunks * 4, st));
     const int fl = fast_len(keys);
     if (t8) {
-        const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)(k * g_stream_table_scale));
+        const uint64_t entries = 1ULL << t8_log2((uint32_t)chunk, (uint32_t)k);
         if (c->st_t8_entries < entries) {
             c->st_t8_entries = 0;
             RBX_TRY(c->st_t8.reserve(entries * 8));
             HIP_TRY(hipMemsetAsync(c->st_t8.p, 0xff, entries * 8, st));
             c->st_t8_entries = entries;
         }
-        RBX_TRY(c->st_occ.reserve(entries / 8));  // written whole by k_stream_occ before it is read
-        if (c->st_flag_bytes < chunk) {
-            c->st_flag_bytes = 0;
-            RBX_TRY(c->st_flag.reserve(chunk));
-            HIP_TRY(hipMemsetAsync(c->st_flag.p, 0, chunk, st));
-            c->st_flag_bytes = chunk;
-        }
     }
-    // The 8-byte table and the owner flags are cleared only when they grow: every chunk's walk and
-    // final pass restore EMPTY / 0.  A launch or memset failing inside the loop breaks that, so the
-    // guard then marks both as uninitialized and the next call clears them again.
+    // The 8-byte table is cleared only when it grows: every chunk's walk restores EMPTY.  A launch
+    // failing inside the loop breaks that, so the guard then marks it as uninitialized and the next
+    // call clears it again.
     struct ResetOnError {
         rbx_ctx *c;
         bool ok = false;
         ~ResetOnError() {
-            if (!ok) c->st_t8_entries = c->st_flag_bytes = 0;
+            if (!ok) c->st_t8_entries = 0;
         }
     } guard{c};
     for (uint64_t base = 0; base < keys.n; base += chunk) {
@@ -1948,23 +1931,11 @@ int rbx_bloom_stream_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nfilter
             s.bb = bb;
             s.pb = pb;
             s.fid_bm = c->fid_table.as<uint32_t *>();
-            s.tkmax = kmax * (uint32_t)g_stream_table_scale;
-            s.flag = c->st_flag.as<uint8_t>();
+            s.tkmax = kmax;
             s.fslot = c->st_fslot.as<uint32_t>();
         }
         s.adds = c->st_adds.as<uint32_t>();
-        s.nadds = c->st_prefilter.as<uint32_t>() + kPrefilterWords + base / chunk;
-        if (g_stream_prefilter) {
-            HIP_TRY(hipMemsetAsync(c->st_prefilter.p, 0, kPrefilterWords * 4, st));
-            s.prefilter = c->st_prefilter.as<uint32_t>();
-            s.pshift = 64 - pbits;
-        } else {
-            s.prefilter = nullptr;
-            if (t8 && g_stream_occ) {  // the table's slot-occupancy bitmap (k_stream_occ), pshift 0
-                s.prefilter = c->st_occ.as<uint32_t>();
-                s.pshift = 0;
-            }
-        }
+        s.nadds = c->st_nadds.as<uint32_t>() + base / chunk;
         s.keys = keys;
         s.base = base;
         s.nchunk = nch;
@@ -2065,7 +2036,7 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
             rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_out, d_counts, c->stream);
         }
         (void)hipEventRecord(c->ev_done[0], c->stream);
-        RBX_TRY(rc);
+        if (rc != RBX_OK) return small_fail(c, rc);
         HIP_TRY(hipMemcpyAsync(sm.hp, sm.dp, (size_t)nseg * 8, hipMemcpyDeviceToHost, c->stream));
         if (out_flags) HIP_TRY(hipMemcpyAsync(sm.tail_h, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2273,7 +2244,7 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         RBX_TRY(small_stage(c, elements, nseg * 4, &sm));
         const int rc = pfadd_run(c, hl, seg_offsets, sm.dk, (uint32_t *)sm.dp, c->stream);
         (void)hipEventRecord(c->ev_done[0], c->stream);
-        RBX_TRY(rc);
+        if (rc != RBX_OK) return small_fail(c, rc);
         HIP_TRY(hipMemcpyAsync(sm.hp, sm.dp, nseg * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         memcpy(ch.data(), sm.hp, nseg * 4);
@@ -3462,20 +3433,24 @@ int rbx_tune(const char *key, int value) {
         g_partition_mode = value;
         return RBX_OK;
     }
-    // DIAGNOSTICS ONLY (tools/microbench.py pflags), results become wrong: 4 = stage 1 emits no
-    // pairs, 8 = the probe records no misses.  0 = normal operation.
-    if (!strcmp(key, "contains_partition_flags")) {
-        if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16 && value != 32 && value != 64)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16, 32, 64}");
-        g_partition_flags = value;
-        return RBX_OK;
-    }
-    // DIAGNOSTICS ONLY (tools/microbench.py padiag), results become wrong: 4 = the region kernel
-    // emits no records, 8 = it loads only its first two regions' pairs (compute floor), 16 = it
-    // only loads (load floor).  0 = normal.
-    if (!strcmp(key, "add_partition_diag")) {
-        if (value < 0 || (value & ~92) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag: bits of 4|8|16|64");
-        g_add_partition_diag = value;
+    // DIAGNOSTICS ONLY, profiling build (kDiag; tools/microbench.py pflags / padiag through RBX_LIB_PATH):
+    // contains_partition_flags 4 = stage 1 emits no pairs, 8 = the probe records no misses, 16 = one
+    // atomicOr per clear bit, 32 = no bit-0 gather, 64 = phase stamps; add_partition_diag 4 = the region
+    // kernel emits no records, 8 = it loads only its first two regions' pairs, 16 = it only loads, 64 =
+    // phase stamps (rbx_bench_add_stamps).  librbx.so rejects them: no knob there changes an answer.
+    if (!strcmp(key, "contains_partition_flags") || !strcmp(key, "add_partition_diag") || !strcmp(key, "stream_diag")) {
+        if (!kDiag) return fail(RBX_E_ILLEGAL_ARGUMENT, std::string(key) + ": diagnostics exist only in librbx_diag.so");
+        if (!strcmp(key, "contains_partition_flags")) {
+            if (value != 0 && value != 4 && value != 8 && value != 12 && value != 16 && value != 32 && value != 64)
+                return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partition_flags in {0, 4, 8, 12, 16, 32, 64}");
+            g_partition_flags = value;
+        } else if (!strcmp(key, "add_partition_diag")) {
+            if (value < 0 || (value & ~92) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_partition_diag: bits of 4|8|16|64");
+            g_add_partition_diag = value;
+        } else {
+            if (value < 0 || (value & ~9) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_diag: bits of 1|8");
+            set_stream_diag(value);
+        }
         return RBX_OK;
     }
     // How the add's region kernel reports which keys are new (add_partitioned.hip k_ba_mode):
@@ -3497,12 +3472,6 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     // EXPERIMENTS (tools/microbench.py): shape and grid of the slot contains kernel (stage 5)
-    if (!strcmp(key, "contains_qshape")) {
-        if (value != 22 && value != 24 && value != 32 && value != 34 && value != 42 && value != 44)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qshape in {22, 24, 32, 34, 42, 44}");
-        set_contains_qshape(value);
-        return RBX_OK;
-    }
     if (!strcmp(key, "stream_table8")) {
         if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_table8 is 0 or 1");
         g_stream_table8 = value;
@@ -3518,27 +3487,6 @@ int rbx_tune(const char *key, int value) {
         g_wide_subchunk = (uint64_t)value;
         return RBX_OK;
     }
-    if (!strcmp(key, "stream_table_scale")) {
-        if (value != 1 && value != 2 && value != 4) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_table_scale in {1, 2, 4}");
-        g_stream_table_scale = value;
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_occupancy")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_occupancy: 0 or 1");
-        g_stream_occ = value;
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_prefilter")) {
-        if (value != 0 && (value < 16 || value > 27))
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_prefilter: 0 or bits in [16, 27]");
-        g_stream_prefilter = value;
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_contains_slots")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_contains_slots in [0, 1]");
-        set_stream_slots(value);
-        return RBX_OK;
-    }
     if (!strcmp(key, "contains_qgrid")) {
         if (value < 256 || value > 8192) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_qgrid in [256, 8192]");
         set_contains_qgrid(value);
@@ -3549,19 +3497,8 @@ int rbx_tune(const char *key, int value) {
         set_stream_qgrid(value);
         return RBX_OK;
     }
-    // DIAGNOSTICS ONLY (timing; answers become wrong): see set_stream_diag
-    if (!strcmp(key, "stream_diag")) {
-        if (value < 0 || (value & ~15) != 0) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_diag: bits of 1|2|4|8");
-        set_stream_diag(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "walk_reset_all")) {
-        if (value < 0 || value > 3) return fail(RBX_E_ILLEGAL_ARGUMENT, "walk_reset_all: bits of 1|2");
-        set_walk_reset_all(value);
-        return RBX_OK;
-    }
     if (!strcmp(key, "add_multi_table8")) {
-        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0, 1 or 2");
+        if (value != 0 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_table8: 0 or 2");
         g_add_multi_t8 = value;
         return RBX_OK;
     }
@@ -3571,7 +3508,7 @@ int rbx_tune(const char *key, int value) {
         return RBX_OK;
     }
     if (!strcmp(key, "add_multi_segmax")) {
-        if (value < 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_segmax >= 1");
+        if (value < 1 || value > (int)kSegMaxKeys) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_segmax in [1, 16384]");
         g_madd_segmax = (uint64_t)value;
         return RBX_OK;
     }
@@ -3580,49 +3517,14 @@ int rbx_tune(const char *key, int value) {
         g_maddx_lgc = (uint32_t)value;
         return RBX_OK;
     }
-    if (!strcmp(key, "stream_owner")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_owner: 0 or 1");
-        set_stream_owner(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_lookup_rounds")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_lookup_rounds: 0 or 1");
-        set_stream_lookup_rounds(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_probe_batch")) {
-        if (value < 0 || value > 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_probe_batch: 0 or 1");
-        set_stream_probe_batch(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "stream_contains_lds")) {
-        if (value < 0 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "stream_contains_lds in [0, 65536]");
-        set_stream_contains_lds(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "contains_stage1_per")) {
-        if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_stage1_per in {1, 2}");
-        set_contains_stage1_per(value);
-        return RBX_OK;
-    }
     if (!strcmp(key, "add_region_grid")) {
         if (value < 256 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_grid in [256, 65536]");
         set_add_region_grid(value);
         return RBX_OK;
     }
-    if (!strcmp(key, "add_region_kernel")) {
-        if (value != 1 && value != 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_region_kernel in {1, 2}");
-        set_add_region_kernel(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "add_multi_seg_lgs")) {
-        if (value != 11 && value != 12) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_seg_lgs in {11, 12}");
-        g_madd_seg_lgs = (uint32_t)value;
-        return RBX_OK;
-    }
-    if (!strcmp(key, "contains_partials")) {
-        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_partials in {0, 1}");
-        g_contains_partials = value;
+    if (!strcmp(key, "add_multi_seg_grid")) {
+        if (value < 64 || value > 65536) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_multi_seg_grid in [64, 65536]");
+        g_madd_seg_grid = (uint32_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "stream_final_grid")) {
@@ -3640,30 +3542,9 @@ int rbx_tune(const char *key, int value) {
         g_small_host = value;
         return RBX_OK;
     }
-    if (!strcmp(key, "add_rebucket_lines")) {
-        if (value < 0 || value > 2) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rebucket_lines in {0, 1, 2}");
-        set_add_rebucket_lines(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "add_stage1_prefetch")) {
-        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_stage1_prefetch in {0, 1}");
-        set_add_stage1_prefetch(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "add_rebucket_prefetch")) {
-        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rebucket_prefetch in {0, 1}");
-        set_add_rebucket_prefetch(value);
-        return RBX_OK;
-    }
     if (!strcmp(key, "add_rec_lds_limit")) {
         if (value < 0 || value > 7168) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_rec_lds_limit in [0, 7168]");
         set_add_rec_lds_limit(value);
-        return RBX_OK;
-    }
-    if (!strcmp(key, "contains_emit2_nt")) {
-        if (value != 512 && value != 1024 && value != 1536 && value != 1792)
-            return fail(RBX_E_ILLEGAL_ARGUMENT, "contains_emit2_nt in {512, 1024, 1536, 1792}");
-        set_contains_emit2_nt(value);
         return RBX_OK;
     }
     if (!strcmp(key, "contains_stage1")) {

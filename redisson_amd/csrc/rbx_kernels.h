@@ -10,6 +10,16 @@ namespace rbx {
 
 constexpr unsigned kMaxGrid = 2048;  // grid-stride cap: 256 CUs x 8 blocks of 256 threads
 
+// Diagnostic switches that make answers wrong (timing A/Bs: rbx_tune "stream_diag",
+// "contains_partition_flags", "add_partition_diag") exist only in the profiling build
+// librbx_diag.so (`make diag`: -DRBX_DIAG=1, used by tools/ through RBX_LIB_PATH).  In librbx.so
+// kDiag is false: every kernel zeroes its diag argument on entry, so those branches are compiled
+// out, and rbx_tune rejects the keys.
+#ifndef RBX_DIAG
+#define RBX_DIAG 0
+#endif
+constexpr bool kDiag = RBX_DIAG != 0;  // grid-stride cap: 256 CUs x 8 blocks of 256 threads
+
 struct KeysDev {
     const uint8_t *bytes;
     const uint64_t *offsets;  // nullable: fixed stride
@@ -107,14 +117,8 @@ inline unsigned grid_for_pc(uint64_t n) {
     return (unsigned)(g < 1 ? 1 : (g > 512 ? 512 : g));
 }
 void launch_contains_partitioned_chunk(const PcArgs &a, int klen_fast, hipStream_t st);
-void set_contains_emit2_nt(int v);  // 512 or 1024 (default)
-void set_contains_stage1_per(int v);  // 1 or 2 (default)
 void set_add_region_grid(int v);  // 256..65536 (default 2048)
-void set_add_region_kernel(int v);  // 1 (r02 8-byte pairs) or 2 (default: 6-byte pairs, pipelined)
 void set_add_rec_lds_limit(int v);  // 0..7168 (tests)
-void set_add_rebucket_prefetch(int v);  // 0 or 1
-void set_add_stage1_prefetch(int v);  // 0 or 1
-void set_add_rebucket_lines(int v);   // 0 k_ba_rebucket, 1 k_ba_emit2 (whole-line runs), 2 by partition count
 
 // partitioned single-filter add (add_partitioned.hip): one chunk of keys
 // Partitioned add: 2^16-bit regions (8 KiB bitmap + two bitsets + a collision table = 32 KiB
@@ -165,8 +169,6 @@ struct StreamChunkArgs {
     unsigned long long *counts;  // [0] present contains, [1] new adds
     uint32_t *adds;       // nchunk: compacted chunk-local positions of the adds
     uint32_t *nadds;      // 1, zeroed per chunk
-    uint32_t *prefilter;  // 2^pbits bits, zeroed per chunk; null: no prefilter (rbx_tune stream_prefilter 0)
-    uint32_t pshift;      // 64 - pbits
     // r04 first-setter table of 8-byte entries (null: the 16-byte epoch-tagged `table` above).
     // entry = (fid << bb | bit) << pb | chunk position, EMPTY = ~0; one CAS claims a bit, and an
     // atomicMin keeps the first setter of a shared one.  Capacity 2^t8_log2(*nadds, kmax), from the
@@ -175,7 +177,6 @@ struct StreamChunkArgs {
     uint32_t bb, pb;              // bits of the largest bitmap's bit index / of a chunk position
     uint32_t tkmax;               // sizes the table: 2^t8_log2(*nadds, tkmax), tkmax = kmax x table scale
     uint32_t *const *fid_bm;      // bitmap words per table id (fid)
-    uint8_t *flag;                // per chunk position: the add owns a bit (zero between chunks; stream_owner 0)
     uint32_t *fslot;              // per add-list entry: the table slot of its first zero bit's claim (r05)
 };
 // state of the optimistic multi-tenant add's conflict table (k_maddx_*), reset per chunk
@@ -210,15 +211,16 @@ struct MaddChunkArgs {
     uint64_t segmax;
 };
 void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st);
-// r05 per-segment multi-tenant add (stream_kernels.hip k_madd_seg): one workgroup per segment, every
-// filter of the batch in one segment only (disjoint bitmaps), k <= 16; segments past segmax keys set
-// *big and are left to the k_maddx_* chunks
+// per-segment multi-tenant add (segment_add.hip k_madd_seg): one 256-thread workgroup per segment, every
+// filter of the batch in one segment only (disjoint bitmaps), k <= 16; segments past segmax (<= kSegMaxKeys)
+// keys set *big and are left to the k_maddx_* chunks
+constexpr uint32_t kSegMaxKeys = 16384;
 struct MaddSegArgs {
     KeysDev keys;
     const FilterDesc *filt;
     const uint64_t *seg_off;
     uint32_t nseg, kmax;
-    uint32_t lgs, tile;       // LDS tables of 2^lgs slots; keys per tile (<= 256)
+    uint32_t grid;            // workgroups (grid-stride over the segments)
     uint64_t segmax;
     uint8_t *out_new;
     unsigned long long *seg_counts;
@@ -236,11 +238,8 @@ __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
 
 // bloom_kernels.hip
 void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st);
-// partials (kMaxGrid words of scratch, or null): per-block counts summed by one small kernel instead of
-// one atomic per block into *count (short kernels: those atomics serialise at the end)
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
-                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st,
-                           unsigned long long *partials = nullptr);
+                           uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
 // tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)
 void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
@@ -274,16 +273,9 @@ void launch_gather_probe(const uint32_t *tbl, uint64_t nwords, uint64_t nkeys, u
                          hipStream_t st);
 
 void set_contains_stage1(int v);
-void set_contains_qshape(int v);  // slot kernel (stage 5): P * 10 + Q
 void set_contains_qgrid(int v);
-void set_stream_slots(int v);  // ordered stream contains: 0 staged, 1 slot kernel
-void set_stream_contains_lds(int v);  // dynamic LDS bytes per stream-contains block (occupancy cap)
-void set_stream_probe_batch(int v);
-void set_stream_diag(int v);
+void set_stream_diag(int v);           // profiling build only (kDiag): bits 1 | 8, see stream_kernels.hip
 void set_stream_final_grid(int v);  // k_stream_final8 blocks (32..2048)
-void set_stream_owner(int v);          // 1 (default) replies from first-claim slots, 0 r04 owner flags
-void set_stream_lookup_rounds(int v);
-void set_walk_reset_all(int v);        // bit 0: stream walk, bit 1: multi-tenant add walk (whole-line resets)  // 1 (default) slot-kernel lookups as slot rounds, 0 inline  // DIAGNOSTICS ONLY (wrong answers): bits 1|2|4|8, see bloom_kernels.hip
 void set_stream_qgrid(int v);  // slot stream-contains kernel grid (blocks)
 int get_contains_stage1();
 

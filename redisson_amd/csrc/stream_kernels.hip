@@ -5,6 +5,8 @@
 // M/ = /root/reference/redisson/src/main/java/org/redisson/
 #include "bloom_common.h"
 
+#include <atomic>
+
 namespace rbx {
 
 // Looks keypart up; ~0u when absent (linear probing never leaves an unclaimed slot before an
@@ -111,27 +113,12 @@ __device__ __forceinline__ uint32_t t8_claim(unsigned long long *__restrict__ T,
 
 // ---- ordered mixed stream (C5): key i is a single-key contains (op 0) or add (op 1) on
 // filters[kf[i]], executed in key order.  Per chunk: compact the adds' positions, probe the adds
-// (first-setter table of add positions per initially-zero bit, plus a prefilter bitset of the
-// (filter, bit) pairs they touch), then the contains -- a zero bit counts as set iff an add at
-// an earlier position of the chunk touches it; the table is consulted only when the prefilter
-// bit is set -- then commit the adds.  Earlier chunks are committed before later ones probe, so
-// chunking keeps the order.  The add list is unordered: owners are resolved by atomicMin.
-// prefilter of 2^pbits bits (rbx_tune "stream_prefilter", default 2^23 = 1 MiB: L2-resident while
-// the contains run, beside the Zipf-hot bitmaps); pshift = 64 - pbits
-__device__ __forceinline__ uint32_t prefilter_bit(uint32_t fid, uint32_t idx, uint32_t pshift) {
-    return (uint32_t)(((((uint64_t)fid << 32) | idx) * 0x9E3779B97F4A7C15ULL) >> pshift);
-}
-
-// May this clear bit have been set by an earlier add of the chunk (look it up in the table)?
-// pshift 0 (r04, with the 8-byte table): `filter` is the occupancy bitmap of the table's slots
-// (k_stream_occ) -- linear probing puts a key at or after its home slot, so an empty home slot
-// means the key is absent; else `filter` is the (fid, bit) prefilter the adds set; NULL: always.
-__device__ __forceinline__ bool maybe_claimed(const uint32_t *__restrict__ filter, uint32_t pshift, uint32_t fid,
-                                              uint32_t idx, uint64_t key8, uint32_t lg8) {
-    if (!filter) return true;
-    const uint64_t b = pshift ? (uint64_t)prefilter_bit(fid, idx, pshift) : t8_slot(key8, lg8);
-    return (filter[b >> 5] >> (b & 31)) & 1u;
-}
+// (first-setter table of add positions per initially-zero bit), then the contains -- a zero bit counts
+// as set iff an add at an earlier position of the chunk claimed it -- then commit the adds.  Earlier
+// chunks are committed before later ones probe, so chunking keeps the order.  The add list is
+// unordered: owners are resolved by atomicMin.  (r03-r05 also carried a (fid, bit) prefilter and a
+// table-occupancy bitmap in front of the lookups; both measured slower on the fresh stream and were
+// removed in r06: profiles/r04/r04g_c5_fresh_prefilter.jsonl, r04o_c5_occupancy_rejected.jsonl.)
 
 // adds[0 .. *nadds) = chunk-local positions of the chunk's adds (any order)
 constexpr uint32_t kCompactPer = 64, kCompactBlock = 256 * kCompactPer;  // commands per lane / per block
@@ -187,8 +174,7 @@ __global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t bas
                                                       const uint32_t *__restrict__ nadds,
                                                       const FilterDesc *__restrict__ filt,
                                                       const uint32_t *__restrict__ kf, HTEntry *__restrict__ T,
-                                                      uint32_t log2cap, uint32_t epoch, uint32_t *__restrict__ zmask,
-                                                      uint32_t *__restrict__ prefilter, uint32_t pshift) {
+                                                      uint32_t log2cap, uint32_t epoch, uint32_t *__restrict__ zmask) {
     const uint32_t na = *nadds;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
@@ -216,10 +202,6 @@ __global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t bas
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
                 zm |= 1u << j;
                 ht_insert(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[j], t);
-                if (prefilter) {
-                    const uint32_t pb = prefilter_bit(f.fid, idxs[j], pshift);
-                    atomicOr(&prefilter[pb >> 5], 1u << (pb & 31));
-                }
             }
         }
         raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
@@ -227,88 +209,28 @@ __global__ __launch_bounds__(256) void k_stream_probe(KeysDev keys, uint64_t bas
     }
 }
 
-template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_stream_contains(KeysDev keys, uint64_t base, uint64_t nchunk,
-                                                         const FilterDesc *__restrict__ filt,
-                                                         const uint32_t *__restrict__ kf,
-                                                         const uint8_t *__restrict__ op,
-                                                         const HTEntry *__restrict__ T, uint32_t log2cap,
-                                                         uint32_t epoch, const uint32_t *__restrict__ prefilter,
-                                                         uint32_t pshift,
-                                                         uint8_t *__restrict__ out,
-                                                         unsigned long long *__restrict__ counts,
-                                                         const unsigned long long *__restrict__ T8, uint32_t bb,
-                                                         uint32_t pb, uint32_t kmax, const uint32_t *__restrict__ nadds) {
-    uint64_t present = 0;
-    const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
-        const uint64_t i = base + t;
-        if (op[i]) continue;
-        const FilterDesc f = filt[kf[i]];
-        uint64_t h1, h2;
-        hash_key<KLEN>(keys, i, h1, h2);
-        // doubling stages 1, 2, 4, ...: all loads of a stage in flight, stop at a clear bit
-        bool all = true;
-        uint64_t h = h1;
-        uint32_t j = 0;
-        for (uint32_t width = 1; j < f.k && all; width <<= 1) {
-            uint32_t word[KMAX], idxs[KMAX];
-            const uint32_t e = min(f.k, j + width);
-#pragma unroll
-            for (int u = 0; u < KMAX; ++u) {
-                if (j + u < e) {
-                    const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                    idxs[u] = idx;
-                    word[u] = f.bm[idx >> 5];
-                    h += ((j + u) & 1) ? h1 : h2;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < KMAX; ++u) {
-                if (j + u < e && all && (word[u] & bit_in_word(idxs[u])) == 0u) {
-                    // set by an earlier add of this chunk?  Only possible if the filter says so.
-                    if (maybe_claimed(prefilter, pshift, f.fid, idxs[u], ((uint64_t)f.fid << bb) | idxs[u], lg8)) {
-                        const uint32_t owner = T8 ? t8_find(T8, lg8, pb, ((uint64_t)f.fid << bb) | idxs[u])
-                                                  : ht_find(T, log2cap, epoch, ((uint64_t)f.fid << 32) | idxs[u]);
-                        all = owner < (uint32_t)t;
-                    } else {
-                        all = false;
-                    }
-                }
-            }
-            j = e;
-        }
-        if (out) out[i] = all;
-        present += all;
-    }
-    if (counts) block_add_u64(present, counts);
-}
-
-// The same answers with the per-lane slot schedule of k_bloom_contains_q (§3.1b): one bit per
+// The chunk's contains with the per-lane slot schedule of k_bloom_contains_q (§3.1b): one bit per
 // key per round trip, P keys in flight per lane.  A wave's queue holds only the chunk's contains
 // commands (ballot-compacted while the wave hashes a 64*Q-command range), so add commands cost
-// no lane time, and a clear bit consults the prefilter / first-setter table exactly as above.
+// no lane time.  (The r02 staged kernel, k_stream_contains, was removed in r06.)
 template <int KLEN, int P, int Q>
 __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_t base, uint64_t nchunk,
                                                            const ProbeDesc *__restrict__ pdesc,
                                                            const uint32_t *__restrict__ kf,
                                                            const uint8_t *__restrict__ op,
                                                            const HTEntry *__restrict__ T, uint32_t log2cap,
-                                                           uint32_t epoch, const uint32_t *__restrict__ prefilter,
-                                                           uint32_t pshift,
-                                                           uint8_t *__restrict__ out,
+                                                           uint32_t epoch, uint8_t *__restrict__ out,
                                                            unsigned long long *__restrict__ counts,
                                                            const unsigned long long *__restrict__ T8, uint32_t bb,
                                                            uint32_t pb, uint32_t kmax,
-                                                           const uint32_t *__restrict__ nadds, uint32_t diag = 0,
-                                                           uint32_t lookup_rounds = 0) {
+                                                           const uint32_t *__restrict__ nadds, uint32_t diag) {
+    if (!kDiag) diag = 0;  // wrong-answer diagnostics exist in the profiling build only (rbx_kernels.h)
     constexpr uint32_t RANGE = 64 * Q, WAVES = 4;
     const uint32_t lg8 = T8 ? t8_log2(*nadds, kmax) : 0;
-    // r05: with the 8-byte table and no prefilter, a clear bit's first-setter lookup is a round of
-    // its own: the slot's next load is the table entry instead of a bitmap word, in flight with
-    // the other slots' gathers (inline, each lookup chain stalled the lane's whole round)
-    const bool rounds = lookup_rounds && T8 && !prefilter && !(diag & 1);
+    // r05: with the 8-byte table a clear bit's first-setter lookup is a round of its own: the slot's
+    // next load is the table entry instead of a bitmap word, in flight with the other slots' gathers
+    // (inline, each lookup chain stalled the lane's whole round).  DIAG bit 1: no lookups.
+    const bool rounds = T8 && !(diag & 1);
     const uint32_t tmask = (uint32_t)((1ULL << lg8) - 1);
     const uint64_t pmask = (1ULL << pb) - 1;
     struct alignas(16) QEnt {
@@ -432,11 +354,8 @@ __global__ __launch_bounds__(256) void k_stream_contains_q(KeysDev keys, uint64_
                         tsl[s] = (uint32_t)t8_slot(((uint64_t)sfid[s] << bb) | sidx[s], lg8);
                         continue;
                     }
-                    if (clear && !(diag & 1)) {  // set by an earlier add of this chunk?  Only if the filter says so.
-                        if (maybe_claimed(prefilter, pshift, sfid[s], sidx[s], ((uint64_t)sfid[s] << bb) | sidx[s], lg8))
-                            clear = !((T8 ? t8_find(T8, lg8, pb, ((uint64_t)sfid[s] << bb) | sidx[s])
-                                          : ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s])) < st[s]);
-                    }
+                    if (clear && !T8 && !(diag & 1))  // set by an earlier add of this chunk (16-byte table)?
+                        clear = !(ht_find(T, log2cap, epoch, ((uint64_t)sfid[s] << 32) | sidx[s]) < st[s]);
                 }
                 bool fin = clear;
                 if (!clear && ((++sjk[s]) & 0xffffu) >= (sjk[s] >> 16)) {
@@ -510,10 +429,8 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
                                                        const uint32_t *__restrict__ nadds,
                                                        const FilterDesc *__restrict__ filt,
                                                        const uint32_t *__restrict__ kf, unsigned long long *__restrict__ T,
-                                                       uint32_t bb, uint32_t pb, uint32_t kmax,
-                                                       uint32_t *__restrict__ prefilter, uint32_t pshift,
-                                                       uint32_t batch, uint32_t *__restrict__ zmask,
-                                                       uint32_t *__restrict__ fslot) {
+                                                       uint32_t bb, uint32_t pb, uint32_t kmax, uint32_t batch,
+                                                       uint32_t *__restrict__ zmask, uint32_t *__restrict__ fslot) {
     const uint32_t na = *nadds;
     const uint32_t lg = t8_log2(na, kmax);
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -540,89 +457,38 @@ __global__ __launch_bounds__(256) void k_stream_probe8(KeysDev keys, uint64_t ba
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
-        if (batch == 2) zm = 0;  // DIAGNOSTIC: no claims
+        if (kDiag && batch == 2) zm = 0;  // DIAGNOSTIC: no claims
         // the slot of the first zero bit's entry: k_stream_final8 decides the reply from it
         const uint32_t fs = t8_claim<KMAX>(T, lg, bb, pb, f.fid, idxs, zm, t, batch);
-        if (zmask) {
-            zmask[a] = zm;
-            fslot[a] = fs;
-        }
-        if (prefilter && pshift) {  // pshift 0: occupancy bitmap, built by k_stream_occ
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if (zm & (1u << j)) {
-                    const uint32_t pb2 = prefilter_bit(f.fid, idxs[j], pshift);
-                    atomicOr(&prefilter[pb2 >> 5], 1u << (pb2 & 31));
-                }
-            }
-        }
+        zmask[a] = zm;
+        fslot[a] = fs;
         raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
     }
 }
 
-// the occupancy bitmap of the table's 2^lg slots (bit s = slot s holds an entry), one ballot per 64
-// slots: streamed after the probe, no atomics (the r03 prefilter cost a memory-side atomicOr per
-// zero bit).  lg >= 12, so every wave's 64 slots exist.
-__global__ __launch_bounds__(256) void k_stream_occ(const unsigned long long *__restrict__ T,
-                                                    const uint32_t *__restrict__ nadds, uint32_t kmax,
-                                                    uint32_t *__restrict__ occ) {
-    const uint64_t nslots = 1ULL << t8_log2(*nadds, kmax);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s - (threadIdx.x & 63) < nslots; s += stride) {
-        const uint64_t m = __ballot(T[s] != ~0ULL);
-        if ((threadIdx.x & 63) == 0) ((unsigned long long *)occ)[s >> 6] = m;
-    }
-}
-
-// every entry: OR its bit into its bitmap, flag its owner, empty the slot (two entries per lane)
+// every entry: OR its bit into its bitmap and empty the slot (two entries per lane).  (r04 also wrote an
+// owner flag per entry for a final pass, and had a whole-line reset variant; both removed in r06.)
 __global__ __launch_bounds__(256) void k_stream_walk(unsigned long long *__restrict__ T, const uint32_t *__restrict__ nadds,
                                                      uint32_t kmax, uint32_t bb, uint32_t pb,
-                                                     uint32_t *const *__restrict__ fid_bm, uint8_t *__restrict__ flag,
-                                                     uint32_t diag = 0, uint32_t reset_all = 0) {
-    // reset_all: every pair is rewritten EMPTY with whole-line streaming stores (at the ~30% loads
-    // the tables run at almost every line holds an entry, and one scattered 16-byte store per
-    // occupied pair cost a partial-line write request each); 0: only occupied pairs are rewritten
+                                                     uint32_t *const *__restrict__ fid_bm) {
     const uint32_t lg = nadds ? t8_log2(*nadds, kmax) : kmax;  // no count: kmax carries lg itself
     const uint64_t n2 = (1ULL << lg) / 2;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t pmask = (1ULL << pb) - 1, bmask = (1ULL << bb) - 1;
+    const uint64_t bmask = (1ULL << bb) - 1;
     using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n2; q += stride) {
         u64x2 e = ((const u64x2 *)T)[q];
-        if ((e.x & e.y) == ~0ULL) {  // both empty
-            if (reset_all) __builtin_nontemporal_store(u64x2{~0ULL, ~0ULL}, (u64x2 *)T + q);
-            continue;
-        }
+        if ((e.x & e.y) == ~0ULL) continue;  // both empty
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const unsigned long long v = h ? e.y : e.x;
             if (v == ~0ULL) continue;
             const uint64_t key = v >> pb;
             const uint32_t bit = (uint32_t)(key & bmask);
-            if (diag & 2) fid_bm[key >> bb][bit >> 5] |= bit_in_word(bit);  // DIAGNOSTIC (racy)
-            else atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
-            if (flag && !(diag & 4)) flag[v & pmask] = 1;
+            atomicOr(&fid_bm[key >> bb][bit >> 5], bit_in_word(bit));
         }
-        if (reset_all) __builtin_nontemporal_store(u64x2{~0ULL, ~0ULL}, (u64x2 *)T + q);
-        else ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
+        ((u64x2 *)T)[q] = u64x2{~0ULL, ~0ULL};
     }
-}
-
-// replies and the new-add count from the owner flags; the flags are cleared for the next chunk
-__global__ __launch_bounds__(256) void k_stream_final(uint64_t base, const uint32_t *__restrict__ adds,
-                                                      const uint32_t *__restrict__ nadds, uint8_t *__restrict__ flag,
-                                                      uint8_t *__restrict__ out, unsigned long long *__restrict__ counts) {
-    uint64_t added = 0;
-    const uint32_t na = *nadds;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += stride) {
-        const uint32_t t = adds[a];
-        const uint8_t v = flag[t];
-        if (v) flag[t] = 0;
-        if (out) out[base + t] = v;
-        added += v;
-    }
-    if (counts) block_add_u64(added, counts + 1);
 }
 
 // r05: replies and the new-add count without owner flags, BEFORE the walk empties the table.  An
@@ -673,97 +539,6 @@ __global__ __launch_bounds__(256) void k_stream_final8(KeysDev keys, uint64_t ba
         added += isnew;
     }
     if (counts) block_add_u64(added, counts + 1);
-}
-
-// ---- multi-tenant add (r05): the stream's 8-byte first-setter table for add(Collection) batches -
-// A multi-tenant add batch (segment s = keys [seg_off[s], seg_off[s+1]) added to filters[s], the
-// segments in order) is the ordered stream with every command an add: key t of a chunk claims its
-// zero bits with entries ((fid << bb | bit) << pb) | t (one CAS each, t8_claim), the reply comes from
-// the entry of its first zero bit (k_madd_final8), and k_stream_walk ORs every owned bit and empties
-// the table.  The r03 path kept 16-byte epoch-tagged entries (a CAS and an atomicMin per zero bit), a
-// commit that re-hashed every key to look its zero bits up again, and one atomicAdd per new key into
-// its segment's count; here the counts are one atomic per (wave, segment).
-template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_madd_probe8(KeysDev keys, uint64_t base, uint64_t nchunk,
-                                                     const FilterDesc *__restrict__ filt,
-                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
-                                                     const uint32_t *__restrict__ tile_seg0,
-                                                     unsigned long long *__restrict__ T, uint32_t lg, uint32_t bb,
-                                                     uint32_t pb, uint32_t batch, uint32_t *__restrict__ zmask,
-                                                     uint32_t *__restrict__ fslot) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nchunk; t += stride) {
-        const uint64_t i = base + t;
-        const FilterDesc f = filt[seg_from(seg_off, nseg, tile_seg0[i >> 8], i)];
-        uint64_t h1, h2;
-        hash_key<KLEN>(keys, i, h1, h2);
-        uint32_t word[KMAX], idxs[KMAX];
-        uint32_t maxidx = 0;
-        uint64_t h = h1;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            if ((uint32_t)j < f.k) {
-                const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                idxs[j] = idx;
-                word[j] = f.bm[idx >> 5];
-                maxidx = idx > maxidx ? idx : maxidx;
-            }
-            h += (j & 1) ? h1 : h2;
-        }
-        uint32_t zm = 0;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
-        const uint32_t fs = t8_claim<KMAX>(T, lg, bb, pb, f.fid, idxs, zm, (uint32_t)t, batch);
-        zmask[t] = zm;
-        fslot[t] = fs;
-        raise_redis_len(f.redis_len, (unsigned long long)(maxidx >> 3) + 1ULL);
-    }
-}
-
-template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_madd_final8(KeysDev keys, uint64_t base, uint64_t nchunk,
-                                                     const FilterDesc *__restrict__ filt,
-                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg,
-                                                     const uint32_t *__restrict__ tile_seg0,
-                                                     const unsigned long long *__restrict__ T, uint32_t lg, uint32_t bb,
-                                                     uint32_t pb, const uint32_t *__restrict__ zmask,
-                                                     const uint32_t *__restrict__ fslot, uint8_t *__restrict__ out_new,
-                                                     unsigned long long *__restrict__ seg_counts) {
-    const uint64_t pmask = (1ULL << pb) - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    // every lane of a wave runs the same number of iterations (wave_seg_add is a wave operation)
-    const uint64_t n_up = (nchunk + 63) & ~63ULL;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_up; t += stride) {
-        const bool in = t < nchunk;
-        const uint64_t i = base + t;
-        uint32_t seg = 0;
-        bool isnew = false;
-        if (in) {
-            seg = seg_from(seg_off, nseg, tile_seg0[i >> 8], i);
-            const uint32_t zm = zmask[t];
-            if (zm) {
-                isnew = (T[fslot[t]] & pmask) == t;
-                const uint32_t rest = zm & (zm - 1);
-                if (!isnew && rest) {  // the first zero bit is shared with an earlier key: the others
-                    const FilterDesc f = filt[seg];
-                    uint64_t h1, h2;
-                    hash_key<KLEN>(keys, i, h1, h2);
-                    uint64_t h = h1;
-#pragma unroll
-                    for (int j = 0; j < KMAX; ++j) {
-                        if (((rest >> j) & 1u) && !isnew) {
-                            const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                            isnew = t8_find(T, lg, pb, ((uint64_t)f.fid << bb) | idx) == (uint32_t)t;
-                        }
-                        h += (j & 1) ? h1 : h2;
-                    }
-                }
-            }
-            if (out_new) out_new[i] = isnew;
-        }
-        if (seg_counts) wave_seg_add(in, seg, isnew ? 1u : 0u, seg_counts);
-    }
 }
 
 // ---- multi-tenant add, r05 default: optimistic SETBITs with conflict repair ---------------------
@@ -1009,239 +784,43 @@ __global__ __launch_bounds__(256) void k_maddx_reset(unsigned long long *__restr
         if (T[s] != ~0ULL) T[s] = ~0ULL;
 }
 
-// ---- multi-tenant add, r05: one workgroup per segment ------------------------------------------
-// When every filter of an add batch appears in one segment only, the segments touch disjoint bitmaps,
-// so a workgroup that owns a segment owns its bitmap for the whole call: no other workgroup reads or
-// writes it, and no memory-side atomic is needed.  The workgroup walks its segment in tiles of TILE
-// keys (one per thread): (1) every key's k words are read -- `sc1` loads, served by this XCD's L2,
-// which holds the previous tile's stores (the vector L1 is not refreshed by stores); (2) its zero bits
-// go into two LDS hash tables: bit -> smallest position of a key meeting it at 0 (CAS + min), word ->
-// the OR of the zero bits and the word as read (every key reads the same value: no store of this tile
-// has happened yet); (3) every word is written back once with a plain store, old | bits; (4) key t is
-// new iff one of its zero bits has t as smallest position.  Tiles run one after another (each sees the
-// previous one's bits), so a key is new iff one of its bits was 0 before the batch and no earlier key
-// of the batch touches it: M/RedissonBloomFilter.java:104-137 in CommandBatchService order.  Segments
-// longer than segmax keys are left to the k_maddx_* chunks (flag `big`).
-template <int KLEN, int KMAX>
-__global__ __launch_bounds__(256) void k_madd_seg(KeysDev keys, const FilterDesc *__restrict__ filt,
-                                                  const uint64_t *__restrict__ seg_off, uint32_t nseg, uint32_t lgs,
-                                                  uint32_t tile, uint64_t segmax, uint8_t *__restrict__ out_new,
-                                                  unsigned long long *__restrict__ seg_counts,
-                                                  uint32_t *__restrict__ big) {
-    extern __shared__ unsigned long long s_dyn[];
-    const uint32_t S = 1u << lgs, smask = S - 1u;
-    unsigned long long *BT = s_dyn;              // bit << 32 | smallest position in the segment; ~0 empty
-    uint32_t *WK = (uint32_t *)(BT + S);         // word index; ~0 empty
-    uint32_t *WV = WK + S;                       // old word | zero bits
-    __shared__ uint32_t s_red[8];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    for (uint32_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
-        const uint64_t a = seg_off[sg], b = seg_off[sg + 1];
-        if (b - a > segmax) {  // uniform: left to the chunked path
-            if (tid == 0) atomicOr(big, 1u);
-            continue;
-        }
-        if (b == a) continue;
-        const FilterDesc f = filt[sg];
-        uint32_t maxidx = 0, nnew = 0;
-        for (uint64_t base = a; base < b; base += tile) {
-            for (uint32_t q = tid; q < S; q += blockDim.x) {
-                BT[q] = ~0ULL;
-                WK[q] = ~0u;
-                WV[q] = 0u;
-            }
-            __syncthreads();
-            const uint64_t i = base + tid;
-            const bool act = tid < tile && i < b;
-            const uint32_t pos = (uint32_t)(i - a);
-            uint32_t idxs[KMAX], word[KMAX], zm = 0;
-            if (act) {
-                uint64_t h1, h2;
-                hash_key<KLEN>(keys, i, h1, h2);
-                uint64_t h = h1;
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    if ((uint32_t)j < f.k) {
-                        const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
-                        idxs[j] = idx;
-                        word[j] = __hip_atomic_load(&f.bm[idx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        maxidx = idx > maxidx ? idx : maxidx;
-                    }
-                    h += (j & 1) ? h1 : h2;
-                }
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j)
-                    if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) zm |= 1u << j;
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    if (!((zm >> j) & 1u)) continue;
-                    const unsigned long long mine = ((unsigned long long)idxs[j] << 32) | pos;
-                    for (uint32_t q = (idxs[j] * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
-                        const unsigned long long o = atomicCAS(&BT[q], ~0ULL, mine);
-                        if (o == ~0ULL) break;
-                        if ((uint32_t)(o >> 32) == idxs[j]) {
-                            if (o > mine) atomicMin(&BT[q], mine);
-                            break;
-                        }
-                    }
-                    const uint32_t w = idxs[j] >> 5;
-                    for (uint32_t q = (w * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
-                        const uint32_t o = atomicCAS(&WK[q], ~0u, w);
-                        if (o == ~0u || o == w) {
-                            atomicOr(&WV[q], word[j] | bit_in_word(idxs[j]));
-                            break;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            for (uint32_t q = tid; q < S; q += blockDim.x) {  // every touched word once, plain stores
-                const uint32_t w = WK[q];
-                if (w != ~0u) f.bm[w] = WV[q];
-            }
-            bool isnew = false;
-            if (act) {
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    if (!((zm >> j) & 1u) || isnew) continue;
-                    for (uint32_t q = (idxs[j] * 0x9E3779B1u) >> (32 - lgs);; q = (q + 1u) & smask) {
-                        const unsigned long long o = BT[q];
-                        if ((uint32_t)(o >> 32) == idxs[j]) {
-                            isnew = (uint32_t)o == pos;
-                            break;
-                        }
-                    }
-                }
-                if (out_new) out_new[i] = isnew;
-            }
-            nnew += isnew;
-            // this tile's stores reach L2 before the next tile's sc1 loads, and the tables are reused
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-        // the segment's count and the Redis string length (every SETBIT grows it to idx / 8 + 1)
-        uint32_t c = nnew, mx = maxidx;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            c += __shfl_down(c, off, 64);
-            mx = max(mx, (uint32_t)__shfl_down(mx, off, 64));
-        }
-        if (lane == 0) {
-            s_red[wave] = c;
-            s_red[4 + wave] = mx;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t tc = 0, tm = 0;
-            for (uint32_t w = 0; w < blockDim.x / 64u; ++w) {
-                tc += s_red[w];
-                tm = max(tm, s_red[4 + w]);
-            }
-            if (tc && seg_counts) atomicAdd(&seg_counts[sg], (unsigned long long)tc);
-            raise_redis_len(f.redis_len, (unsigned long long)(tm >> 3) + 1ULL);
-        }
-        __syncthreads();  // s_red reuse
-    }
-}
-
-template <int KLEN>
-static void launch_madd_seg_len(const MaddSegArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)(8 + 4 + 4) << a.lgs;
-    const dim3 grid(std::min<uint32_t>(a.nseg, 4096));
-    if (a.kmax <= 8)
-        hipLaunchKernelGGL((k_madd_seg<KLEN, 8>), grid, dim3(256), lds, st, a.keys, a.filt, a.seg_off, a.nseg, a.lgs,
-                           a.tile, a.segmax, a.out_new, a.seg_counts, a.big);
-    else
-        hipLaunchKernelGGL((k_madd_seg<KLEN, 16>), grid, dim3(256), lds, st, a.keys, a.filt, a.seg_off, a.nseg, a.lgs,
-                           a.tile, a.segmax, a.out_new, a.seg_counts, a.big);
-}
-
-void launch_madd_seg(const MaddSegArgs &a, int klen_fast, hipStream_t st) {
-    switch (klen_fast) {
-    case 16: launch_madd_seg_len<16>(a, st); break;
-    case 32: launch_madd_seg_len<32>(a, st); break;
-    case 64: launch_madd_seg_len<64>(a, st); break;
-    default: launch_madd_seg_len<0>(a, st); break;
-    }
-}
-
-static int g_stream_slots = 1;  // rbx_tune("stream_contains_slots"): 0 staged kernel, 1 slot kernel (default)
-void set_stream_slots(int v) { g_stream_slots = v; }
 // The slot stream kernel at P = 2, Q = 2 (120 VGPRs, four blocks per CU) on 1024 blocks, one
 // resident round: C5 9.91 (2048) -> 9.67 ms; shapes 32 / 42 / 24: 10.8 / 11.2 / 11.2 ms
-// (profiles/r03/r03u_c5sweep_qshape_qgrid.jsonl).
-static unsigned g_stream_qgrid = 1024;
+// (profiles/r03/r03u_c5sweep_qshape_qgrid.jsonl).  rbx_tune "stream_qgrid".
+static std::atomic<unsigned> g_stream_qgrid{1024};
 void set_stream_qgrid(int v) { g_stream_qgrid = (unsigned)v; }
-// k_stream_contains runs best at four 256-thread blocks per CU (4 waves/SIMD): the Zipf-hot
-// tenants' bitmaps live in L2, and more resident waves interleave more tenants.  Its registers
-// (93 VGPRs since the r02 hash) would admit five, so the launch reserves 33,000 bytes of dynamic
-// LDS per block (four fit in 160 KiB).  C5, same box: 11.28 -> 10.99 ms per 1e8 commands; three
-// blocks per CU: 0.66 ms per chunk vs 0.545 (profiles/r02/r02ze_c5_occupancy.txt).
-// rbx_tune("stream_contains_lds") overrides the bytes (0: registers decide).
-static int g_stream_lds = 33000;
-void set_stream_contains_lds(int v) { g_stream_lds = v; }
-// k_stream_probe8: 1 (default) every zero bit's home-slot CAS issued before any is waited on, 0 one
-// claim after another (rbx_tune "stream_probe_batch")
-static uint32_t g_probe8_batch = 1;
-void set_stream_probe_batch(int v) { g_probe8_batch = (uint32_t)v; }
-// DIAGNOSTICS ONLY (timing; answers become wrong): 1 = the stream contains skip the first-setter
-// lookups, 2 = the walk ORs bits with plain read-modify-writes, 4 = the walk writes no owner flags,
-// 8 = the probe makes no claims
-static uint32_t g_stream_diag = 0;
+// DIAGNOSTICS ONLY, profiling build (kDiag; answers become wrong): 1 = the stream contains skip the
+// first-setter lookups, 8 = the probe makes no claims
+static std::atomic<uint32_t> g_stream_diag{0};
 void set_stream_diag(int v) { g_stream_diag = (uint32_t)v; }
-// r05 (rbx_tune "stream_owner"): 1 (default) replies from the first claims' slots (k_stream_final8),
-// 0 the r04 owner flags written by the walk (k_stream_final)
-static int g_stream_owner = 1;
-void set_stream_owner(int v) { g_stream_owner = v; }
-// r05 (rbx_tune "stream_lookup_rounds"): 1 (default) the slot contains kernel issues a first-setter
-// lookup as one more round of its slot (in flight with the other slots' gathers), 0 inline
-static uint32_t g_stream_lookup_rounds = 1;
-void set_stream_lookup_rounds(int v) { g_stream_lookup_rounds = (uint32_t)v; }
-// rbx_tune "walk_reset_all": bit 0 = the stream's walk rewrites every pair (whole lines), bit 1 =
-// the multi-tenant add's walk does
-static uint32_t g_walk_reset_all = 0;
-void set_walk_reset_all(int v) { g_walk_reset_all = (uint32_t)v; }
 // rbx_tune "stream_final_grid": k_stream_final8's blocks.  Each block adds its new-add count to ONE counter,
 // and same-address atomics serialise: 2048 / 512 / 256 blocks 39.3 / 28.3 / 35.6 us per C5 chunk (r05as).
-static unsigned g_final8_grid = 512;
+static std::atomic<unsigned> g_final8_grid{512};
 void set_stream_final_grid(int v) { g_final8_grid = (unsigned)v; }
 
+// One chunk: compact -> probe (8-byte claims, or the 16-byte table when (fid, bit) does not fit 41 bits)
+// -> slot contains -> replies from the first claims (k_stream_final8) + walk, or the 16-byte commit.
 template <int KLEN, int KMAX>
 static void launch_stream_chunk_k(const StreamChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(a.nchunk, kMaxGrid);
     const unsigned cgrid = (unsigned)((a.nchunk + kCompactBlock - 1) / kCompactBlock);
+    const uint32_t diag = kDiag ? g_stream_diag.load() : 0u;
     hipLaunchKernelGGL(k_stream_compact, dim3(cgrid ? cgrid : 1), dim3(256), 0, st, a.op, a.base, a.nchunk, a.adds,
                        a.nadds);
-    const bool own8 = a.t8 && g_stream_owner == 1;  // r05: replies from the first claims, no flags
     if (a.t8)
         hipLaunchKernelGGL((k_stream_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.prefilter, a.pshift,
-                           (g_stream_diag & 8) ? 2u : g_probe8_batch, own8 ? a.zmask : nullptr,
-                           own8 ? a.fslot : nullptr);
+                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, (diag & 8) ? 2u : 1u, a.zmask, a.fslot);
     else
         hipLaunchKernelGGL((k_stream_probe<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.prefilter, a.pshift);
-    if (a.t8 && a.prefilter && a.pshift == 0)  // occupancy filter of the 8-byte table
-        hipLaunchKernelGGL(k_stream_occ, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.prefilter);
-    if (g_stream_slots)
-        hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid)), dim3(256), 0, st,
-                           a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter,
-                           a.pshift, a.out, a.counts, a.t8, a.bb, a.pb, a.tkmax, a.nadds, g_stream_diag,
-                           g_stream_lookup_rounds);
-    else
-        hipLaunchKernelGGL((k_stream_contains<KLEN, KMAX>), dim3(grid), dim3(256), g_stream_lds, st, a.keys, a.base, a.nchunk,
-                           a.filt, a.kf, a.op, a.table, a.log2cap, a.epoch, a.prefilter, a.pshift, a.out, a.counts,
-                           a.t8, a.bb, a.pb, a.tkmax, a.nadds);
-    if (own8) {
-        hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(std::min(grid, g_final8_grid)), dim3(256), 0, st, a.keys,
-                           a.base, a.adds, a.nadds,
-                           a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.zmask, a.fslot, a.out, a.counts);
-        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
-                           (uint8_t *)nullptr, g_stream_diag, g_walk_reset_all & 1u);
-    } else if (a.t8) {
-        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm,
-                           a.flag, g_stream_diag, g_walk_reset_all & 1u);
-        hipLaunchKernelGGL(k_stream_final, dim3(grid), dim3(256), 0, st, a.base, a.adds, a.nadds, a.flag, a.out, a.counts);
+                           a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask);
+    hipLaunchKernelGGL((k_stream_contains_q<KLEN, 2, 2>), dim3(std::min(grid, g_stream_qgrid.load())), dim3(256), 0, st,
+                       a.keys, a.base, a.nchunk, a.pdesc, a.kf, a.op, a.table, a.log2cap, a.epoch, a.out, a.counts,
+                       a.t8, a.bb, a.pb, a.tkmax, a.nadds, diag);
+    if (a.t8) {
+        hipLaunchKernelGGL((k_stream_final8<KLEN, KMAX>), dim3(std::min(grid, g_final8_grid.load())), dim3(256), 0, st,
+                           a.keys, a.base, a.adds, a.nadds, a.filt, a.kf, a.t8, a.bb, a.pb, a.tkmax, a.zmask, a.fslot,
+                           a.out, a.counts);
+        hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, a.nadds, a.tkmax, a.bb, a.pb, a.fid_bm);
     } else {
         hipLaunchKernelGGL((k_stream_commit<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.adds, a.nadds,
                            a.filt, a.kf, a.table, a.log2cap, a.epoch, a.zmask, a.out, a.counts);
@@ -1256,18 +835,6 @@ static void launch_stream_chunk_len(const StreamChunkArgs &a, hipStream_t st) {
 }
 
 template <int KLEN, int KMAX>
-static void launch_madd8_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
-    const unsigned grid = grid_for(a.nchunk, kMaxGrid);
-    hipLaunchKernelGGL((k_madd_probe8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.seg_off, a.nseg, a.tile_seg0, a.t8, a.lg, a.bb, a.pb, g_probe8_batch, a.zmask, a.fslot);
-    hipLaunchKernelGGL((k_madd_final8<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.seg_off, a.nseg, a.tile_seg0, a.t8, a.lg, a.bb, a.pb, a.zmask, a.fslot, a.out_new,
-                       a.seg_counts);
-    hipLaunchKernelGGL(k_stream_walk, dim3(kMaxGrid), dim3(256), 0, st, a.t8, (const uint32_t *)nullptr, a.lg, a.bb,
-                       a.pb, a.fid_bm, (uint8_t *)nullptr, 0u, (g_walk_reset_all >> 1) & 1u);
-}
-
-template <int KLEN, int KMAX>
 static void launch_maddx_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
     const unsigned grid = grid_for(std::max<uint64_t>(a.nchunk, 1ULL << a.lgC), kMaxGrid);
     hipLaunchKernelGGL((k_maddx_gather<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
@@ -1275,8 +842,8 @@ static void launch_maddx_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_maddx_set<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
                        a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.bb, a.pb, a.cst, a.big);
     hipLaunchKernelGGL((k_maddx_claim<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
-                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst,
-                       g_probe8_batch, a.big);
+                       a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst, 1u,
+                       a.big);
     hipLaunchKernelGGL((k_maddx_reply<KLEN, KMAX>), dim3(grid), dim3(256), 0, st, a.keys, a.base, a.nchunk, a.filt,
                        a.seg_off, a.nseg, a.tile_seg0, a.zmask, a.c8, a.lgC, a.t8, a.lg, a.bb, a.pb, a.cst, a.out_new,
                        a.seg_counts, a.big, a.segmax);
@@ -1285,15 +852,9 @@ static void launch_maddx_chunk_k(const MaddChunkArgs &a, hipStream_t st) {
 
 template <int KLEN>
 static void launch_madd8_chunk_len(const MaddChunkArgs &a, hipStream_t st) {
-    if (a.c8) {
-        if (a.kmax <= 8) launch_maddx_chunk_k<KLEN, 8>(a, st);
-        else if (a.kmax <= 16) launch_maddx_chunk_k<KLEN, 16>(a, st);
-        else launch_maddx_chunk_k<KLEN, 32>(a, st);
-        return;
-    }
-    if (a.kmax <= 8) launch_madd8_chunk_k<KLEN, 8>(a, st);
-    else if (a.kmax <= 16) launch_madd8_chunk_k<KLEN, 16>(a, st);
-    else launch_madd8_chunk_k<KLEN, 32>(a, st);
+    if (a.kmax <= 8) launch_maddx_chunk_k<KLEN, 8>(a, st);
+    else if (a.kmax <= 16) launch_maddx_chunk_k<KLEN, 16>(a, st);
+    else launch_maddx_chunk_k<KLEN, 32>(a, st);
 }
 
 void launch_madd8_chunk(const MaddChunkArgs &a, int klen_fast, hipStream_t st) {

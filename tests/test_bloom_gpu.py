@@ -338,7 +338,7 @@ def test_multi_tenant_parity(client, fresh, small):
         client.getBloomFilter(n).delete()
 
 
-@pytest.mark.parametrize("table8,clog2", [(2, 17), (2, 6), (1, 17), (0, 17)])
+@pytest.mark.parametrize("table8,clog2", [(2, 17), (2, 6), (0, 17)])
 @pytest.mark.parametrize("chunk", [0, 700])
 def test_multi_tenant_add_first_setter_tables(client, fresh, table8, clog2, chunk):
     """r05: multi-tenant add(Collection) by optimistic SETBITs with conflict repair (add_multi_table8 2,
@@ -388,20 +388,21 @@ def test_multi_tenant_add_first_setter_tables(client, fresh, table8, clog2, chun
 
 
 ADD_MULTI_DEFAULT = 2
-ADD_MULTI_SEG_LGS_DEFAULT = 12
+ADD_MULTI_SEG_GRID_DEFAULT = 8192
 
 
-@pytest.mark.parametrize("segmax,lgs", [(16384, 12), (300, 12), (1, 12), (16384, 11)])
+@pytest.mark.parametrize("segmax,grid", [(16384, 8192), (300, 8192), (1, 8192), (16384, 64)])
 @pytest.mark.parametrize("fixed", [True, False])
-def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, lgs, fixed):
-    """r05: a multi-tenant add whose filters are all distinct runs one workgroup per segment (k_madd_seg:
-    LDS first setters, plain word stores, tiles of <= 256 keys in order); segments longer than
-    add_multi_segmax keys go to the chunked path in the same call (segmax 300: both paths; 1: every
-    non-trivial segment chunked).  40 filters with k = 3..16 (KMAX 8 and 16), 1..1,500 keys per segment
-    (many tiles per segment), keys repeated within a segment and across tile boundaries
-    (shared zero bits), fixed 16-byte or variable-length keys.  Per-key flags, per-segment counts and every
-    bitmap vs the oracle; then the same batch again (every key already present)."""
-    rng = np.random.default_rng(1300 + segmax + int(fixed))
+def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, grid, fixed):
+    """A multi-tenant add whose filters are all distinct runs one workgroup per segment (k_madd_seg: tiles
+    of <= 256 keys in order, LDS first setters, plain word stores, the next tile's hash before the store
+    wait); segments longer than add_multi_segmax keys go to the chunked path in the same call (segmax
+    300: both paths; 1: every non-trivial segment chunked); grid 64: workgroups walk many segments.
+    40 filters with k = 3..16 (KMAX 8 and 16; tiles of 160..256 keys), 1..1,500 keys per segment, keys
+    repeated within a segment and across tile boundaries (shared zero bits), fixed 16-byte or
+    variable-length keys.  Per-key flags, per-segment counts and every bitmap vs the oracle; then the
+    same batch again (every key already present)."""
+    rng = np.random.default_rng(1300 + segmax + grid + int(fixed))
     nt = 40
     names = [f"{fresh}-{t}" for t in range(nt)]
     refs = []
@@ -424,7 +425,7 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, lgs, fix
         keys = [pool[int(j)] for j in rng.integers(0, len(pool), size=n)]
         arena, sub = Arena(keys), (lambda a, b: O.arena(keys[a:b]))
     assert L.lib().rbx_tune(b"add_multi_segmax", segmax) == 0
-    assert L.lib().rbx_tune(b"add_multi_seg_lgs", lgs) == 0  # 11: 2^11 LDS slots, full at tile x kmax = 2048
+    assert L.lib().rbx_tune(b"add_multi_seg_grid", grid) == 0
     try:
         for rep in range(2):
             counts, flags = bloom_add_multi(client, handles, segs, arena, per_key=True)
@@ -436,13 +437,65 @@ def test_multi_tenant_add_one_segment_per_filter(client, fresh, segmax, lgs, fix
                 assert int(counts.sum()) > n // 4
     finally:
         L.lib().rbx_tune(b"add_multi_segmax", 16384)
-        L.lib().rbx_tune(b"add_multi_seg_lgs", ADD_MULTI_SEG_LGS_DEFAULT)
+        L.lib().rbx_tune(b"add_multi_seg_grid", ADD_MULTI_SEG_GRID_DEFAULT)
     for nm, r in zip(names, refs):
         assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
     for h in handles:
         h.close()
     for nm in names:
         client.getBloomFilter(nm).delete()
+
+
+@pytest.mark.parametrize("fill", [0.5, 0.0])
+def test_multi_tenant_add_segment_tile_boundaries(client, fresh, fill):
+    """k = 10 (tryInit(1e6, 1e-3): 14,377,587 bits) tenants whose segments hold
+    exactly 1, 255, 256, 257, 511, 512, 513, 1024, 1025 and 16,384 keys (the per-segment kernel's tile
+    is 256 keys at k = 10; 16,384 = add_multi_segmax, the longest segment it takes), fresh 16-byte keys
+    plus repeats of keys from earlier tiles of the same segment.  fill 0.5: bitmaps at design fill (~5
+    zero bits per key); fill 0: empty bitmaps (10 zero bits per key: the LDS tables at their 0.625 load
+    bound).  Per-key flags, counts and every bitmap vs the oracle (M/RedissonBloomFilter.java:104-137)."""
+    import torch
+
+    rng = np.random.default_rng(0x5E6B + int(fill * 10))
+    sizes = [1, 255, 256, 257, 511, 512, 513, 1024, 1025, 16384]
+    names = [f"{fresh}:{t}" for t in range(len(sizes))]
+    nb = (14_377_587 + 7) // 8
+    refs, handles = [], []
+    try:
+        for nm in names:
+            f = client.getBloomFilter(nm)
+            assert f.tryInit(1_000_000, 1e-3)
+            r = O.OracleBloom(14_377_587, 10)
+            if fill:
+                bm = rng.integers(0, 256, size=nb, dtype=np.uint8)
+                d = torch.from_numpy(bm).cuda()
+                assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), d.data_ptr(), nb, None) == 0
+                torch.cuda.synchronize()
+                del d
+                r.bitmap[:nb] = bm
+                r.redis_len = nb
+            refs.append(r)
+            handles.append(BloomHandle(client, nm))
+        segs = np.zeros(len(sizes) + 1, np.uint64)
+        segs[1:] = np.cumsum(sizes)
+        n = int(segs[-1])
+        keys = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+        for t, sz in enumerate(sizes):  # repeats: a key of an earlier round again (and one inside a round)
+            a = int(segs[t])
+            for p in range(1, sz, 97):
+                keys[a + p] = keys[a + int(rng.integers(0, p))]
+        counts, flags = bloom_add_multi(client, handles, segs, Arena.fixed(keys), per_key=True)
+        for t in range(len(sizes)):
+            a, b = int(segs[t]), int(segs[t + 1])
+            c, fl = refs[t].add(*O.fixed_arena(keys[a:b]), per_key=True)
+            assert counts[t] == c and np.array_equal(flags[a:b], fl), (t, sizes[t])
+        for nm, r in zip(names, refs):
+            assert client.getBloomFilter(nm).exportBitmap() == r.redis_string(), nm
+    finally:
+        for h in handles:
+            h.close()
+        for nm in names:
+            client.getBloomFilter(nm).delete()
 
 
 @pytest.mark.parametrize("segment", [1, 0])
@@ -494,7 +547,7 @@ def test_multi_tenant_add_segment_path_at_c3_shape(client, fresh, segment):
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("table8", [2, 1, 0])
+@pytest.mark.parametrize("table8", [2, 0])
 def test_multi_tenant_add_filter_ids_past_2_17(client, fresh, table8):
     """per-key add parity of a multi-tenant add batch whose filter ids reach 2^17:
     100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10) at design fill, one add_multi batch of
@@ -601,12 +654,10 @@ def test_full_size_2pow32_property(client, fresh):
     f.delete()
 
 
-@pytest.mark.parametrize("flags", [0, 16])
-def test_partitioned_contains_miss_record_overflow(client, fresh, flags):
+def test_partitioned_contains_miss_record_overflow(client, fresh):
     """A half-full filter with k = 16 probed by absent keys: ~3.75 clear bits per key, so the
     probe's per-region LDS record list (4096) and the per-range record capacity (2 per key)
-    both overflow into the direct atomicOr path; flags 16 takes the direct path for every clear
-    bit.  Per-key answers equal the oracle's either way."""
+    both overflow into the direct atomicOr path.  Per-key answers equal the oracle's."""
     from redisson_amd import _lib as L_
 
     rng = np.random.default_rng(31)
@@ -620,12 +671,10 @@ def test_partitioned_contains_miss_record_overflow(client, fresh, flags):
     ref.redis_len = size // 8
     probe = rng.integers(0, 256, size=(1_500_000, 16), dtype=np.uint8)
     assert L_.lib().rbx_tune(b"contains_partition", 1) == 0
-    assert L_.lib().rbx_tune(b"contains_partition_flags", flags) == 0
     try:
         cg, pg = f.containsEach(Arena.fixed(probe))
     finally:
         L_.lib().rbx_tune(b"contains_partition", 2)
-        L_.lib().rbx_tune(b"contains_partition_flags", 0)
     cr, pr = ref.contains(*O.fixed_arena(probe), per_key=True)
     assert cg == cr and np.array_equal(pg, pr)
     f.delete()
@@ -774,20 +823,12 @@ def test_contains_multi_schedules_identical(client, fresh, sched, varlen):
         client.getBloomFilter(nm).delete()
 
 
-@pytest.mark.parametrize("slots", [0, 1])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_mixed_stream_in_order_semantics(client, fresh, seed, slots):
+def test_mixed_stream_in_order_semantics(client, fresh, seed):
     """C5 shape: an ordered stream of single-key contains/add commands over tenants with a
     skewed tenant choice; every answer equals the one-after-another oracle replay, including
-    contains right after an add of the same key and adds racing on shared bits.  Both contains
-    kernels (staged, slots)."""
-    from redisson_amd import _lib as L
-
-    assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
-    try:
-        _stream_case(client, fresh, seed)
-    finally:
-        L.lib().rbx_tune(b"stream_contains_slots", 1)
+    contains right after an add of the same key and adds racing on shared bits."""
+    _stream_case(client, fresh, seed)
 
 
 def _stream_case(client, fresh, seed):
@@ -1075,14 +1116,13 @@ def test_partitioned_add_collision_table_rounds(client, fresh, records):
     f.delete()
 
 
-@pytest.mark.parametrize("tune", [(b"add_rec_lds_limit", 0), (b"add_rec_lds_limit", 64), (b"add_region_kernel", 1)])
+@pytest.mark.parametrize("tune", [(b"add_rec_lds_limit", 0), (b"add_rec_lds_limit", 64)])
 @pytest.mark.parametrize("records", [1, 3])
 def test_partitioned_add_region_variants(client, fresh, tune, records):
     """The region pass's other branches give the oracle's answers too: owner records past the
     block's LDS record space (add_rec_lds_limit 0 / 64: every region, or most, reports its owners by
-    direct atomics instead of record runs), the r02 kernel on 8-byte region pairs
-    (add_region_kernel 1).  Two batches, the second re-adding and repeating keys; flags, counts,
-    bitmap bytes and count() equal the in-order SETBIT fold."""
+    direct atomics instead of record runs).  Two batches, the second re-adding and repeating keys;
+    flags, counts, bitmap bytes and count() equal the in-order SETBIT fold."""
     from redisson_amd import _lib as L_
 
     rng = np.random.default_rng(4242 + records)
@@ -1105,7 +1145,6 @@ def test_partitioned_add_region_variants(client, fresh, tune, records):
         L_.lib().rbx_tune(b"add_partition", 2)
         L_.lib().rbx_tune(b"add_records", 2)
         L_.lib().rbx_tune(b"add_rec_lds_limit", 7168)
-        L_.lib().rbx_tune(b"add_region_kernel", 2)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()
@@ -1134,78 +1173,6 @@ def test_partitioned_add_overflow_falls_back(client, fresh):
     assert cg == cr and np.array_equal(ng, nr)
     assert f.exportBitmap() == ref.redis_string()
     f.delete()
-
-
-ADD_REBUCKET_LINES_DEFAULT = 0
-
-
-@pytest.mark.parametrize("records", [1, 3, 0])
-def test_partitioned_add_whole_line_rebucket(client, fresh, records):
-    """r05 k_ba_emit2 (rbx_tune add_rebucket_lines 1, forced at every size): whole-line region runs,
-    remainders carried between tiles and a partition's last runs padded with pairs the region pass
-    skips.  Shapes of test_partitioned_add_parity (power-of-two and odd sizes, k 3..16, fixed and
-    variable-length keys), each with a batch that repeats keys within itself and re-adds earlier
-    ones; then the collision-table shape (every key twice in one region) and the overflow fallback.
-    Per-key flags, counts, bitmap bytes and count() vs the oracle."""
-    from redisson_amd import _lib as L_
-
-    assert L_.lib().rbx_tune(b"add_partition", 1) == 0
-    assert L_.lib().rbx_tune(b"add_records", records) == 0
-    assert L_.lib().rbx_tune(b"add_rebucket_lines", 1) == 0
-    try:
-        for j, (size, k, L) in enumerate([(1 << 32, 7, 32), (300_000_007, 10, 16), ((1 << 29) + 3, 16, 0),
-                                          (1 << 20, 3, 24)]):
-            rng = np.random.default_rng(9000 + 7 * j + records)
-            n = 200_000
-            if L:
-                mat = rng.integers(0, 256, size=(n, L), dtype=np.uint8)
-                second = np.concatenate([mat[n // 8: n // 2], mat[rng.integers(0, n // 2, size=n // 4)], mat[n // 2:]])
-                arenas = [(Arena.fixed(mat[: n // 4]), O.fixed_arena(mat[: n // 4])),
-                          (Arena.fixed(second), O.fixed_arena(second))]
-            else:
-                keys = [rng.bytes(int(x)) for x in rng.integers(0, 90, size=n)]
-                second = keys[n // 8: n // 2] + [keys[i] for i in rng.integers(0, n // 2, size=n // 4)] + keys[n // 2:]
-                arenas = [(Arena(keys[: n // 4]), O.arena(keys[: n // 4])), (Arena(second), O.arena(second))]
-            nm = f"{fresh}-{j}"
-            f = client.getBloomFilter(nm)
-            f.tryInitRaw(size, k)
-            ref = O.OracleBloom(size, k)
-            for a, o in arenas:
-                cg, ng = f.addEach(a)
-                cr, nr = ref.add(*o, per_key=True)
-                assert cg == cr and np.array_equal(ng, nr), (size, k, L)
-            assert f.exportBitmap() == ref.redis_string(), (size, k, L)
-            assert f.count() == ref.count()
-            f.delete()
-        # every key twice in one 2^16-bit region (collision-table rounds)
-        rng = np.random.default_rng(78 + records)
-        base = rng.integers(0, 256, size=(420, 24), dtype=np.uint8)
-        batch = np.concatenate([base, base[::-1], rng.integers(0, 256, size=(3, 24), dtype=np.uint8)])
-        f = client.getBloomFilter(f"{fresh}-c")
-        f.tryInitRaw(1 << 16, 7)
-        ref = O.OracleBloom(1 << 16, 7)
-        for b in (batch, batch[::3]):
-            cg, ng = f.addEach(Arena.fixed(b))
-            cr, nr = ref.add(*O.fixed_arena(b), per_key=True)
-            assert cg == cr and np.array_equal(ng, nr)
-        assert f.exportBitmap() == ref.redis_string()
-        f.delete()
-        # overflow: 40 keys repeated 400k times -> the chunk reruns on the first-setter table
-        base = rng.integers(0, 256, size=(40, 32), dtype=np.uint8)
-        batch = np.concatenate([base[rng.integers(0, 40, size=400_000)],
-                                rng.integers(0, 256, size=(30_000, 32), dtype=np.uint8)])
-        f = client.getBloomFilter(f"{fresh}-o")
-        f.tryInitRaw(1 << 30, 7)
-        ref = O.OracleBloom(1 << 30, 7)
-        cg, ng = f.addEach(Arena.fixed(batch))
-        cr, nr = ref.add(*O.fixed_arena(batch), per_key=True)
-        assert cg == cr and np.array_equal(ng, nr)
-        assert f.exportBitmap() == ref.redis_string()
-        f.delete()
-    finally:
-        L_.lib().rbx_tune(b"add_partition", 2)
-        L_.lib().rbx_tune(b"add_records", 2)
-        L_.lib().rbx_tune(b"add_rebucket_lines", ADD_REBUCKET_LINES_DEFAULT)
 
 
 def test_cross_stream_calls_run_in_call_order(client, fresh):
@@ -1371,11 +1338,11 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     keys = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
     keys[n - 1000:] = keys[:1000]  # repeats inside the batch
     dk = device_keys(keys.data_ptr(), n, 32)
-    # (add_partition, add_records, add_rebucket_lines): the whole-line rebucket with both report kinds
-    runs = [(0, 2, 0), (1, 0, 0), (1, 1, 0), (1, 3, 0), (1, 1, 1), (1, 3, 1)]
+    # (add_partition, add_records)
+    runs = [(0, 2), (1, 0), (1, 1), (1, 3)]
     flags, counts, bitmaps = [], [], []
     try:
-        for i, (part, rec, lines) in enumerate(runs):
+        for i, (part, rec) in enumerate(runs):
             nm = f"{fresh}-{i}"
             f = client.getBloomFilter(nm)
             f.tryInitRaw(1 << 32, 7)
@@ -1384,7 +1351,6 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
             out = torch.zeros((2, n), dtype=torch.uint8, device="cuda")
             L.lib().rbx_tune(b"add_partition", part)
             L.lib().rbx_tune(b"add_records", rec)
-            assert L.lib().rbx_tune(b"add_rebucket_lines", lines) == 0
             for j in range(2):  # second pass: every key already present
                 h.add_dev(dk, cnt.data_ptr() + 8 * j, out[j].data_ptr())
             torch.cuda.synchronize()
@@ -1396,7 +1362,6 @@ def test_partitioned_add_record_kinds_agree_at_c2_scale(client, fresh):
     finally:
         L.lib().rbx_tune(b"add_partition", 2)
         L.lib().rbx_tune(b"add_records", 2)
-        L.lib().rbx_tune(b"add_rebucket_lines", ADD_REBUCKET_LINES_DEFAULT)
     assert counts[0][1] == 0 and n - 1000 - 10 <= counts[0][0] <= n - 1000, counts[0]
     for i in range(1, len(runs)):
         assert counts[i] == counts[0], (runs[i], counts[i], counts[0])

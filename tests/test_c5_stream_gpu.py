@@ -18,10 +18,6 @@ from redisson_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 
-# the engine's defaults (rbx_bench.h rbx_tune), restored after a case that overrides them
-STREAM_SLOTS_DEFAULT = 1
-STREAM_PREFILTER_DEFAULT = 0
-STREAM_TABLE_SCALE_DEFAULT = 1
 
 
 def _zipf_tenants(rng, nt, n, s=1.0):
@@ -31,9 +27,7 @@ def _zipf_tenants(rng, nt, n, s=1.0):
     return np.minimum(np.searchsorted(cdf, rng.random(n)), nt - 1).astype(np.uint32)
 
 
-def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, klen=64, prefilter=None, table8=None,
-             occupancy=None, probe_batch=None, table_scale=None, hot_last=False, geometry=None, owner=None,
-             lookup_rounds=None):
+def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, klen=64, table8=None, hot_last=False, geometry=None):
     """expected: one tryInit size for every tenant, or a per-tenant list.  hot_last: the Zipf-hottest
     tenant is the LAST handle (the largest filter id of the call) instead of the first.  geometry:
     the (bb, fbits, pb, chunk) the call must have run with (rbx_bench_stream_geometry)."""
@@ -56,7 +50,7 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
     if hot_last:
         first, last = kf == 0, kf == nt - 1
         kf[first], kf[last] = nt - 1, 0
-    if nt > 1 << 16:  # ids past 2^16 (the tag's filter-id field, the prefilter hash) really occur
+    if nt > 1 << 16:  # ids past 2^16 (the tag's filter-id field) really occur
         assert int(kf.max()) >= 1 << 16 and np.count_nonzero(kf >= 1 << 8) > n // 4
     op = (rng.random(n) < 0.1).astype(np.uint8)
     pool = rng.integers(0, 256, size=(n // 4, klen), dtype=np.uint8)
@@ -67,22 +61,8 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
     kf[idx + 1] = kf[idx]
     keys[idx + 1] = keys[idx]
     assert L.lib().rbx_tune(b"stream_chunk", chunk) == 0
-    if slots is not None:
-        assert L.lib().rbx_tune(b"stream_contains_slots", slots) == 0
-    if prefilter is not None:
-        assert L.lib().rbx_tune(b"stream_prefilter", prefilter) == 0
     if table8 is not None:
         assert L.lib().rbx_tune(b"stream_table8", table8) == 0
-    if occupancy is not None:
-        assert L.lib().rbx_tune(b"stream_occupancy", occupancy) == 0
-    if probe_batch is not None:
-        assert L.lib().rbx_tune(b"stream_probe_batch", probe_batch) == 0
-    if table_scale is not None:
-        assert L.lib().rbx_tune(b"stream_table_scale", table_scale) == 0
-    if owner is not None:
-        assert L.lib().rbx_tune(b"stream_owner", owner) == 0
-    if lookup_rounds is not None:
-        assert L.lib().rbx_tune(b"stream_lookup_rounds", lookup_rounds) == 0
     try:
         out, counts = bloom_stream(client, handles, kf, op, _fixed(keys))
         if geometry is not None:
@@ -91,14 +71,7 @@ def _c5_case(client, fresh, seed, nt, expected, fpp, n, chunk=0, slots=None, kle
             assert tuple(int(x) for x in g) == tuple(geometry), (g, geometry)
     finally:
         L.lib().rbx_tune(b"stream_chunk", 0)
-        L.lib().rbx_tune(b"stream_contains_slots", STREAM_SLOTS_DEFAULT)
-        L.lib().rbx_tune(b"stream_prefilter", STREAM_PREFILTER_DEFAULT)
         L.lib().rbx_tune(b"stream_table8", 1)
-        L.lib().rbx_tune(b"stream_occupancy", 0)
-        L.lib().rbx_tune(b"stream_probe_batch", 1)
-        L.lib().rbx_tune(b"stream_table_scale", STREAM_TABLE_SCALE_DEFAULT)
-        L.lib().rbx_tune(b"stream_owner", 1)
-        L.lib().rbx_tune(b"stream_lookup_rounds", 1)
     want, wc = O.bloom_stream(refs, kf, op, keys, None, stride=klen)
     bad = np.flatnonzero(out != want)
     assert bad.size == 0, (bad.size, bad[:10], out[bad[:10]], want[bad[:10]], kf[bad[:10]], op[bad[:10]])
@@ -131,45 +104,19 @@ def test_c5_instantiation_two_full_chunks(client, fresh):
     _c5_case(client, fresh, seed=0x5EED0005, nt=200, expected=1_000_000, fpp=1e-3, n=14_000_000)
 
 
-@pytest.mark.parametrize("prefilter", [0, 21, 25])
-@pytest.mark.parametrize("slots", [0, 1])
-def test_c5_kmax8_many_chunks(client, fresh, slots, prefilter):
+def test_c5_kmax8_many_chunks(client, fresh):
     """k = 7 tenants (tryInit(1e6, 0.01): 9,585,058 bits -> k_stream_*<64, 8>), 64-byte keys, 2M commands
-    in 300k-command chunks; both contains kernels (staged, per-lane slots), with and without the
-    prefilter in front of the first-setter table."""
-    _c5_case(client, fresh, seed=77 + slots + 2 * prefilter, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000,
-             chunk=300_000, slots=slots, prefilter=prefilter)
+    in 300k-command chunks."""
+    _c5_case(client, fresh, seed=77, nt=64, expected=1_000_000, fpp=0.01, n=2_000_000, chunk=300_000)
 
 
-@pytest.mark.parametrize("probe_batch", [0, 1])
-def test_c5_probe_claims_batched_or_serial(client, fresh, probe_batch):
-    """The 8-byte table's claims: every home-slot CAS of an add in flight at once (1, default) or one
-    after another (0); hot tenants (Zipf, 120 of them) make shared bits and occupied home slots
-    common within a chunk, so the atomicMin and the serial probe-on paths both run."""
-    _c5_case(client, fresh, seed=616 + probe_batch, nt=120, expected=1_000_000, fpp=1e-3, n=1_400_000,
-             chunk=350_000, probe_batch=probe_batch)
-
-
-@pytest.mark.parametrize("owner", [1, 0])
-@pytest.mark.parametrize("lookup_rounds", [1, 0])
-@pytest.mark.parametrize("slots", [1, 0])
-def test_c5_owner_replies_and_lookup_rounds(client, fresh, owner, lookup_rounds, slots):
-    """r05: add replies from the slot of each add's first zero-bit claim (stream_owner 1, default;
-    k_stream_final8 runs before the walk) or from the r04 owner flags (0); first-setter lookups as
-    rounds of the slot kernel (stream_lookup_rounds 1, default) or inline (0); both contains kernels.
-    Keys repeat (a quarter of the stream is distinct) and 80 Zipf tenants share bits within a chunk,
-    so an add's first zero bit is often claimed by an earlier add (final8's slow path) and many
-    contains meet a bit claimed earlier in the chunk (the lookup round finds it)."""
-    _c5_case(client, fresh, seed=929 + 4 * owner + 2 * lookup_rounds + slots, nt=80, expected=1_000_000, fpp=1e-3,
-             n=1_200_000, chunk=400_000, slots=slots, owner=owner, lookup_rounds=lookup_rounds)
-
-
-@pytest.mark.parametrize("scale", [1, 2, 4])
-def test_c5_table_scale(client, fresh, scale):
-    """The 8-byte table at 1x / 2x / 4x its entries (rbx_tune stream_table_scale): claims, lookups and
-    the walk follow the same 2^t8_log2 on every kernel; exact against the oracle."""
-    _c5_case(client, fresh, seed=717 + scale, nt=100, expected=1_000_000, fpp=1e-3, n=900_000, chunk=300_000,
-             table_scale=scale)
+def test_c5_shared_bits_and_claimed_lookups(client, fresh):
+    """Add replies from the slot of each add's first zero-bit claim (k_stream_final8, before the walk)
+    and first-setter lookups as rounds of the slot contains kernel.  Keys repeat (a quarter of the
+    stream is distinct) and 80 Zipf tenants share bits within a chunk, so an add's first zero bit is
+    often claimed by an earlier add (final8's slow path), occupied home slots make claims probe on, and
+    many contains meet a bit claimed earlier in the chunk (the lookup round finds it)."""
+    _c5_case(client, fresh, seed=929, nt=80, expected=1_000_000, fpp=1e-3, n=1_200_000, chunk=400_000)
 
 
 @pytest.mark.parametrize("table8", [0, 1])
@@ -180,16 +127,6 @@ def test_c5_first_setter_tables_agree(client, fresh, table8):
              table8=table8)
 
 
-@pytest.mark.parametrize("occupancy", [0, 1])
-@pytest.mark.parametrize("slots", [0, 1])
-def test_c5_table_occupancy_filter(client, fresh, occupancy, slots):
-    """Without a prefilter, a clear bit is looked up in the 8-byte first-setter table only when its
-    home slot is occupied (k_stream_occ's bitmap, 1) or always (0, default): both contains kernels,
-    small chunks (many occupancy passes), exact against the oracle."""
-    _c5_case(client, fresh, seed=515 + 2 * occupancy + slots, nt=150, expected=1_000_000, fpp=1e-3, n=1_200_000,
-             chunk=200_000, slots=slots, prefilter=0, occupancy=occupancy)
-
-
 def test_c5_k10_chunk_boundaries(client, fresh):
     """C5 tenants and keys in 303,031-command chunks (= 101 * 3000 + 1: the add at 303,030 and the
     contains of the same key at 303,031 sit on the two sides of the first boundary; the earlier
@@ -197,27 +134,27 @@ def test_c5_k10_chunk_boundaries(client, fresh):
     _c5_case(client, fresh, seed=91, nt=100, expected=1_000_000, fpp=1e-3, n=2_000_000, chunk=303_031)
 
 
-@pytest.mark.parametrize("prefilter", [23, 0])
-def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, prefilter):
-    """C5's tenant count.  The first-setter tags and the prefilter hash carry the
-    filter's index in the call (up to 2^17 here), so the bench leg's id range is checked against the
-    oracle too: 100,000 tryInit(1000, 1e-3) tenants (14,377 bits, k = 10 -> the same <64, 16>
-    instantiation as C5, 1.8 KB each), Zipf(1.0) tenants, 10% adds, 64-byte keys, 2.1M commands in
-    three chunks, with a 2^23-bit prefilter and without it (the default) (every clear bit looked up in
-    the table).  Per-command replies, both counts and every tenant's bitmap must be identical."""
+@pytest.mark.parametrize("table8", [1, 0])
+def test_c5_100k_tenants_filter_ids_past_2_17(client, fresh, table8):
+    """C5's tenant count.  The first-setter entries carry the filter's index in the call
+    (up to 2^17 here), so the bench leg's id range is checked against the oracle too: 100,000
+    tryInit(1000, 1e-3) tenants (14,377 bits, k = 10 -> the same <64, 16> instantiation as C5, 1.8 KB
+    each), Zipf(1.0) tenants, 10% adds, 64-byte keys, 2.1M commands in three chunks, on the 8-byte table
+    (1) and the 16-byte fallback (0).  Per-command replies, both counts and every tenant's bitmap must be
+    identical."""
     f = client.getBloomFilter(fresh + "-probe")
     f.tryInit(1000, 1e-3)
     assert (f.getSize(), f.getHashIterations()) == (14_377, 10)
     f.delete()
-    wc = _c5_case(client, fresh, seed=0xC5100 + prefilter, nt=100_000, expected=1000, fpp=1e-3, n=2_100_000,
-                  chunk=700_000, prefilter=prefilter)
+    wc = _c5_case(client, fresh, seed=0xC5100 + 23 * (1 - table8), nt=100_000, expected=1000, fpp=1e-3, n=2_100_000,
+                  chunk=700_000, table8=table8)
     assert wc[1] > 10_000
 
 
 @pytest.mark.parametrize("table8", [1, 0])
 def test_stream_k20_variable_keys(client, fresh, table8):
     """The stream's KMAX = 32 instantiation and variable-length keys (KLEN = 0: the generic hash
-    path of the probe, both contains kernels and the 8-byte table): tryInit(10_000, 1e-6) tenants
+    path of the probe, the slot contains kernel and both first-setter tables): tryInit(10_000, 1e-6) tenants
     (k = 20), keys of 0..90 bytes, adds and contains of the same keys interleaved, 3 chunks."""
     rng = np.random.default_rng(0xC520 + table8)
     from redisson_amd import Arena

@@ -333,41 +333,16 @@ def main():
         h.close()
         fb.delete()
 
-    if "palines" in a.what:
-        # r05: the add's rebucket with whole-line runs (k_ba_emit2) vs k_ba_rebucket, n/2 keys into an
-        # empty 2^32-bit filter, interleaved, fresh filter per run; new-key counts must agree
-        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
-        m = n // 2
-        res, news = {0: [], 1: []}, {0: set(), 1: set()}
-        for rnd in range(4):
-            for ln in res:
-                assert L.lib().rbx_tune(b"add_rebucket_lines", ln) == 0
-                fb = client.getBloomFilter(f"pl-{rnd}-{ln}")
-                fb.tryInitRaw(1 << 32, 7)
-                h = BloomHandle(client, f"pl-{rnd}-{ln}")
-                cnt.zero_()
-                res[ln].append(timed(stream, lambda: h.add_dev(device_keys(keys.data_ptr(), m, 32), cnt.data_ptr(),
-                                                                stream=sp), 1))
-                news[ln].add(int(cnt[0].item()))
-                h.close()
-                fb.delete()
-        L.lib().rbx_tune(b"add_rebucket_lines", 0)
-        assert news[0] == news[1] and len(news[0]) == 1, news
-        for ln, v in res.items():
-            print(json.dumps({"bench": "add_rebucket_lines", "lines": ln, "ms": v, "ms_median": statistics.median(v),
-                              "new": min(news[ln])}), flush=True)
-
     if "regstamp" in a.what:
-        # region-pass phase times (add_partition_diag 64, exact results) of each region kernel,
-        # C2 add of n/2 keys into an empty 2^32-bit filter; summed over blocks, in ms of one CU's
-        # wave 0 (s_memtime ticks at 100 MHz) per block slot
+        # region-pass phase times (add_partition_diag 64, exact results; the profiling build:
+        # RBX_LIB_PATH=redisson_amd/librbx_diag.so), C2 add of n/2 keys into an empty 2^32-bit filter;
+        # summed over blocks, in ms of one CU's wave 0 (s_memtime ticks at 100 MHz) per block slot
         import ctypes as C
 
         cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
         m = n // 2
         names = ["top_wait", "setup", "prefetch", "pass1", "pass2", "table", "owners", "writeback"]
-        for rk in (1, 2, 1, 2):
-            assert L.lib().rbx_tune(b"add_region_kernel", rk) == 0
+        for rk in (2, 2):
             assert L.lib().rbx_tune(b"add_partition_diag", 64) == 0
             fb = client.getBloomFilter(f"rs-{rk}")
             fb.tryInitRaw(1 << 32, 7)
@@ -388,7 +363,6 @@ def main():
             h.close()
             fb.delete()
         L.lib().rbx_tune(b"add_partition_diag", 0)
-        L.lib().rbx_tune(b"add_region_kernel", 2)
 
     if "pcstamp" in a.what:
         # partitioned contains phase times (contains_partition_flags 64, exact results), C2 contains
@@ -576,9 +550,8 @@ def main():
                 fb.delete()
                 for kv in filter(None, ("" if v == "-" else v).split(",")):
                     key = kv.split("=")[0]
-                    L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2, "add_region_kernel": 2,
-                                                       "add_region_grid": 2048, "add_rec_lds_limit": 7168,
-                                                       "add_rebucket_prefetch": 1, "add_stage1_prefetch": 1}.get(key, 0))
+                    L.lib().rbx_tune(key.encode(), {"add_records": 2, "add_partition": 2, "add_region_grid": 2048,
+                                                       "add_rec_lds_limit": 7168}.get(key, 0))
         assert len(set(news.values())) == 1, news
         for v, t in res.items():
             med = statistics.median(t)
@@ -716,7 +689,7 @@ def main():
 
     if "c3ab" in a.what:
         # C3 set up once (bench.py run_c3 shape), then contains kernels interleaved round by round
-        # in one process: RBX_C3AB="stage1:shape:grid,..." (shape/grid only used by stage 5)
+        # in one process: RBX_C3AB="stage1:grid,..." (grid only used by stage 5)
         import ctypes as C
 
         import numpy as np
@@ -741,7 +714,7 @@ def main():
         arr = (C.c_void_p * nt)(*[h.h.value for h in hs])
         dk = device_keys(k16.data_ptr(), m, 16)
         variants = [tuple(int(x) for x in v.split(":")) for v in
-                    os.environ.get("RBX_C3AB", "4:0:0,5:42:2048,5:22:2048").split(",")]
+                    os.environ.get("RBX_C3AB", "4:0,5:2048,5:1024").split(",")]
 
         def run():
             assert L.lib().rbx_bloom_contains_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
@@ -754,8 +727,7 @@ def main():
                 L.lib().rbx_tune(b"contains_stage1", v[0])
                 L.lib().rbx_tune(b"contains_multi_slots", 1 if v[0] == 5 else 0)
                 if v[0] == 5:
-                    L.lib().rbx_tune(b"contains_qshape", v[1])
-                    L.lib().rbx_tune(b"contains_qgrid", v[2])
+                    L.lib().rbx_tune(b"contains_qgrid", v[1])
                 counts.zero_()
                 run()
                 c = counts.clone()
@@ -766,8 +738,62 @@ def main():
         L.lib().rbx_tune(b"contains_multi_slots", 2)
         for v, t in res.items():
             med = statistics.median(t)
-            print(json.dumps({"bench": "c3ab", "stage1": v[0], "shape": v[1], "grid": v[2], "ms_median": med,
+            print(json.dumps({"bench": "c3ab", "stage1": v[0], "grid": v[1], "ms_median": med,
                               "ms_min": min(t), "ms_max": max(t), "keys_per_s": m / (med / 1e3)}), flush=True)
+        for h in hs:
+            h.close()
+
+    if "c3add" in a.what:
+        # C3's add half (bench.py c3_add_half shape: 1,000 fresh 16-byte keys per tenant per call, filters at
+        # design fill) with the per-segment kernel shapes interleaved call by call in one process:
+        # RBX_C3ADD="grid,..." (rbx_tune add_multi_seg_grid), every call on a new key window
+        import ctypes as C
+
+        import numpy as np
+
+        nt = int(os.environ.get("RBX_C3_TENANTS", "100000"))
+        pool = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+        rng = np.random.default_rng(0)
+        hs = []
+        for t in range(nt):
+            nm = f"aa:{t:06d}"
+            f = client.getBloomFilter(nm)
+            f.tryInit(1_000_000, 1e-3)
+            nbytes = (f._size + 7) // 8
+            off = int(rng.integers(0, (pool.numel() - nbytes) // 256)) * 256
+            assert L.lib().rbx_bloom_import_dev(client.ctx, nm.encode(), pool.data_ptr() + off, nbytes, sp) == 0
+            hs.append(BloomHandle(client, nm))
+        del pool
+        per = max(1, n // nt)
+        m = per * nt
+        variants = [int(x) for x in os.environ.get("RBX_C3ADD", "8192,4096").split(",")]
+        rounds = int(os.environ.get("RBX_C3ADD_ROUNDS", "5"))
+        ncalls = rounds * len(variants) + 1
+        k16 = torch.randint(0, 256, (m + ncalls * per, 16), dtype=torch.uint8, device="cuda", generator=g)
+        seg = torch.arange(nt + 1, dtype=torch.int64, device="cuda") * per
+        counts = torch.zeros(nt, dtype=torch.int64, device="cuda")
+        arr = (C.c_void_p * nt)(*[h.h.value for h in hs])
+        call = [0]
+
+        def run():
+            dk = device_keys(k16.data_ptr() + 16 * per * call[0], m, 16)
+            call[0] += 1
+            assert L.lib().rbx_bloom_add_multi_dev(client.ctx, arr, nt, seg.data_ptr(), C.byref(dk), None,
+                                                    counts.data_ptr(), sp) == 0
+
+        run()  # warm
+        res = {v: [] for v in variants}
+        for rnd in range(rounds):
+            for v in variants:
+                assert L.lib().rbx_tune(b"add_multi_seg_grid", v) == 0
+                counts.zero_()
+                res[v].append(timed(stream, run, 1))
+                assert int(counts.sum().item()) > m * 0.99
+        L.lib().rbx_tune(b"add_multi_seg_grid", 8192)
+        for v, t in res.items():
+            med = statistics.median(t)
+            print(json.dumps({"bench": "c3add", "seg_grid": v, "ms_median": med, "ms_min": min(t), "ms_max": max(t),
+                              "keys_per_s": m / (med / 1e3)}), flush=True)
         for h in hs:
             h.close()
 

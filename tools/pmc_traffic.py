@@ -36,7 +36,7 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
          ("k_stream_final", r"k_stream_final\("), ("k_madd_probe8", r"k_madd_probe8<"),
          ("k_madd_final8", r"k_madd_final8<"), ("k_maddx_gather", r"k_maddx_gather<"),
          ("k_maddx_set", r"k_maddx_set<"), ("k_maddx_claim", r"k_maddx_claim<"), ("k_maddx_reply", r"k_maddx_reply<"),
-         ("k_maddx_reset", r"k_maddx_reset"), ("k_madd_seg", r"k_madd_seg<"),
+         ("k_maddx_reset", r"k_maddx_reset"), ("k_madd_seg", r"k_madd_seg<"), ("k_madd_tiles", r"k_madd_tiles<"),
          ("k_stream_contains_q", r"k_stream_contains_q<"),
          ("k_stream_contains", r"k_stream_contains<"),
          ("k_stream_commit", r"k_stream_commit<"),
@@ -50,7 +50,7 @@ SHORT = [("k_bk_stage1", r"k_bk_stage1<"), ("k_bk_emit2", r"k_bk_emit2<"), ("k_b
 CLASS = {"k_bk_stage1": "mixed", "k_bloom_contains": "mixed", "k_bloom_contains_multi": "mixed",
          "k_bloom_contains_q": "mixed", "k_stream_probe": "mixed", "k_stream_contains": "mixed",
          "k_stream_contains_q": "mixed",
-         "k_stream_commit": "mixed", "k_stream_probe8": "mixed", "k_madd_probe8": "mixed", "k_maddx_gather": "mixed", "k_madd_seg": "mixed", "k_gather_probe": "gather",
+         "k_stream_commit": "mixed", "k_stream_probe8": "mixed", "k_madd_probe8": "mixed", "k_maddx_gather": "mixed", "k_madd_seg": "mixed", "k_madd_tiles": "mixed", "k_gather_probe": "gather",
          "k_bloom_add_probe": "gather",
          "k_bloom_add_commit": "gather"}  # every other kernel: stream
 
