@@ -101,3 +101,21 @@ def test_negative_expected_insertions_like_the_reference():
         want = O.bloom_optimal(n, p)
         assert (s.value, k.value) == want, (n, p, s.value, k.value, want)
         assert s.value < 0
+
+
+def test_product_library_has_no_wrong_answer_switches():
+    """the timing diagnostics that make answers wrong exist only in the profiling build
+    (librbx_diag.so, `make diag`); librbx.so rejects their keys, and the r02-r05 A/B variants removed in
+    r06 are gone with their knobs.  The whitelist (include/rbx_bench.h) still answers."""
+    lib = L.lib()
+    for key in (b"stream_diag", b"contains_partition_flags", b"add_partition_diag"):
+        assert lib.rbx_tune(key, 1 if key == b"stream_diag" else 4) == -1, key
+        assert "profiling build" in L.last_error() or "librbx_diag" in L.last_error()
+    for key in (b"stream_prefilter", b"stream_occupancy", b"stream_owner", b"stream_contains_slots",
+                b"walk_reset_all", b"contains_qshape", b"contains_partials", b"add_rebucket_lines",
+                b"add_region_kernel", b"add_multi_seg_lgs", b"stream_table_scale", b"contains_emit2_nt"):
+        assert lib.rbx_tune(key, 1) == -1, key
+    assert lib.rbx_tune(b"add_multi_table8", 1) == -1
+    for key, val in ((b"add_multi_table8", 2), (b"contains_stage1", 4), (b"stream_table8", 1),
+                     (b"add_multi_seg_grid", 8192), (b"host_small_bytes", 4 << 20)):
+        assert lib.rbx_tune(key, val) == 0, key
