@@ -766,7 +766,7 @@ def main():
         del pool
         per = max(1, n // nt)
         m = per * nt
-        variants = [int(x) for x in os.environ.get("RBX_C3ADD", "8192,4096").split(",")]
+        variants = [tuple(int(y) for y in x.split(":")) for x in os.environ.get("RBX_C3ADD", "8192,4096").split(",")]
         rounds = int(os.environ.get("RBX_C3ADD_ROUNDS", "5"))
         ncalls = rounds * len(variants) + 1
         k16 = torch.randint(0, 256, (m + ncalls * per, 16), dtype=torch.uint8, device="cuda", generator=g)
@@ -785,7 +785,9 @@ def main():
         res = {v: [] for v in variants}
         for rnd in range(rounds):
             for v in variants:
-                assert L.lib().rbx_tune(b"add_multi_seg_grid", v) == 0
+                assert L.lib().rbx_tune(b"add_multi_seg_grid", v[0]) == 0
+                if len(v) > 1:  # "grid:tune_value" with RBX_C3ADD_KEY naming the knob
+                    assert L.lib().rbx_tune(os.environ["RBX_C3ADD_KEY"].encode(), v[1]) == 0
                 counts.zero_()
                 res[v].append(timed(stream, run, 1))
                 assert int(counts.sum().item()) > m * 0.99
