@@ -12,12 +12,12 @@ RBX_STREAM_BYTES="k_bk_stage1=3.2e9 k_bloom_contains=3.2e9" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c2" --workload c2 || exit 1
 fi
 if [[ ",$ONLY," == *",c3,"* ]]; then
-RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9 k_maddx_gather=1.333e8 k_madd_probe8=1.333e8 k_madd_seg=1.6e9" \
+RBX_STREAM_BYTES="k_bloom_contains_q=1.6e9 k_bloom_contains_multi=1.6e9 k_maddx_gather=1.333e8 k_madd_seg=1.6e9" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c3" --workload c3 || exit 1
 fi
 [[ ",$ONLY," == *",c4,"* ]] && { timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c4" --workload c4 || exit 1 ; }
 if [[ ",$ONLY," == *",c5,"* ]]; then
-RBX_STREAM_BYTES="k_stream_contains_q=4.84e8 k_stream_contains=4.84e8 k_stream_probe=5.37e7 k_stream_probe8=5.37e7 k_stream_commit=5.37e7" \
+RBX_STREAM_BYTES="k_stream_contains_q=4.84e8 k_stream_probe=5.37e7 k_stream_probe8=5.37e7 k_stream_commit=5.37e7" \
   timeout -k 10 1200 bash "$R/tools/profile_round.sh" "${TAG}_c5" --workload c5 || exit 1
 fi
 python3 - "$R/gpurun_out" "$TAG" <<'PY'
