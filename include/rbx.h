@@ -237,7 +237,10 @@ int rbx_bloom_add_dev(rbx_ctx *ctx, rbx_bloom *b, const rbx_keys *d_keys, uint8_
 int rbx_bloom_contains_multi_dev(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
                                  const uint64_t *d_seg_offsets, const rbx_keys *d_keys,
                                  uint8_t *d_out_present, unsigned long long *d_counts, void *stream);
-/* add() per segment, segments applied in order (same semantics as nseg calls). */
+/* add() per segment, segments applied in order (same semantics as nseg calls).  Enqueued on `stream`;
+ * when every filter of the batch is distinct and the batch holds more than 16,384 keys, the call waits
+ * for its per-segment kernel (one flag read back) to learn whether a segment that long needs the
+ * chunked path (M/RedissonBloomFilter.java:104-137). */
 int rbx_bloom_add_multi_dev(rbx_ctx *ctx, rbx_bloom *const *filters, uint32_t nseg,
                             const uint64_t *d_seg_offsets, const rbx_keys *d_keys,
                             uint8_t *d_out_new, unsigned long long *d_counts, void *stream);
