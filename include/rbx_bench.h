@@ -89,6 +89,13 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           0: every host batch on the pipelined copy-stream path
  *   "host_small_bytes"      that path's limit: key bytes (+ offsets), 4 KiB .. 64 MiB (default
  *                           4 MiB; at most a quarter as many keys)
+ *   "host_tiny_keys"        host-arena batches of at most this many keys (0..16384, default 16384)
+ *                           and 64 KiB of key bytes run from coherent pinned memory: the kernel reads
+ *                           the keys over the host link and writes the flags back, one launch and one
+ *                           sync (adds also within add_single_seg_keys); 0: the one-transfer path
+ *   "add_single_seg_keys"   single-filter adds of at most this many keys with k <= 16 (0..16384,
+ *                           default 256) run the per-segment kernel on one segment (one launch, first
+ *                           setters in LDS) instead of the table path; 0: the table path
  * Profiling build only (librbx_diag.so, `make diag`; librbx.so rejects them): "stream_diag",
  * "contains_partition_flags", "add_partition_diag" -- timing diagnostics that make answers wrong
  * (rbx_kernels.h kDiag).  Removed in r06 with the variants they selected (measured slower, never

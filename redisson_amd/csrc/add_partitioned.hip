@@ -323,15 +323,8 @@ __global__ __launch_bounds__(kBaRbThreads) void k_ba_rebucket(const unsigned lon
     ps.flush(stamps);
 }
 
-// B' (r05) ------------------------------------------------------------------------------
-// The rebucket with whole-line runs (the shape of contains_partitioned.hip's k_bk_emit2): one block
-// per stage-1 partition, its tiles in order, every run a multiple of kBaLine pairs (two 64-byte lines
-// of lo words + one of hi halves), each fine bucket's remainder carried in LDS (6-byte form) to the
-// next tile, and a partition's last remainders padded to a whole line with kBaPadHi pairs, which the
-// region pass skips.  k_ba_rebucket's runs start and end mid-line: ~12M of its 45M write requests at
-// C2 are partial lines (profiles/r04/r04p_c2), and a partial line costs a whole request.  Few
-// partitions (C1: 48) would leave most CUs idle, so the launcher keeps k_ba_rebucket there.
-constexpr uint32_t kBaLine = 32;
+// The r05 whole-line rebucket (k_ba_emit2), which padded a partition's last runs with kBaPadHi pairs, was
+// removed in r06; the region pass still skips such pairs, which nothing emits now.
 constexpr uint16_t kBaPadHi = 0xffffu;  // hi half of a padding pair: real keys are < 2^26 (hi < 1024)
 static_assert(kBaMaxRegionPairs <= 65536, "region pair counts fit the LDS counters");
 

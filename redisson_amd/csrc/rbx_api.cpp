@@ -241,6 +241,9 @@ struct rbx_ctx {
     size_t pin_small_cap = 0;
     uint64_t pin_small_limit = 0;  // the host_small_bytes the block was laid out for (its tail offset)
     unsigned long long *pin_word = nullptr;  // pinned readback words (counts, the partitioned add's overflow flag)
+    // tiny host batches (bloom_host_tiny): coherent pinned memory the kernel reads the keys from and
+    // writes the flags into, no transfer on either side
+    uint8_t *pin_tiny = nullptr, *pin_tiny_dev = nullptr;
 
     // stream order of the scratch above across calls issued on different streams (ScratchOrder)
     hipEvent_t ev_scratch = nullptr;
@@ -699,10 +702,35 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
     return RBX_OK;
 }
 
+// Small single-filter adds (<= add_single_seg_keys keys, k <= 16): the per-segment kernel on one segment --
+// one workgroup, the batch's first setters in LDS (§3.9) -- instead of the table path's memset, probe and
+// commit: one launch.  Its plain word stores need the bitmap to itself, which the context's call order
+// gives (every call waits for the previous one's stream, ScratchOrder).
+static std::atomic<uint64_t> g_seg_single_keys{256};  // rbx_tune("add_single_seg_keys"): 0 = off
+
+static bool use_seg_single(const FilterDesc &f, uint64_t n, uint64_t lim) { return f.k <= 16 && n <= lim; }
+
+static void launch_seg_single(const KeysDev &keys, const FilterDesc &f, uint8_t *d_out_new,
+                              unsigned long long *d_count, hipStream_t st) {
+    MaddSegArgs a{};
+    a.keys = keys;
+    a.single = f;
+    a.kmax = f.k;
+    a.segmax = kSegMaxKeys;  // >= keys.n: the `big` flag stays unused
+    a.out_new = d_out_new;
+    a.seg_counts = d_count;
+    launch_madd_seg(a, fast_len(keys), st);
+}
+
 static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, const uint64_t *d_seg_off,
                    uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
                    unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
     if (keys.n == 0) return RBX_OK;
+    if (d_filt == nullptr && use_seg_single(single, keys.n, g_seg_single_keys)) {
+        launch_seg_single(keys, single, d_out_new, d_count, st);
+        HIP_TRY(hipGetLastError());
+        return RBX_OK;
+    }
     if (d_filt == nullptr && use_add_partitioned(single.mp.size, single.k, keys.n))
         return run_add_partitioned(c, keys, single, d_out_new, d_count, st);
     return run_add_table(c, keys, d_filt, d_seg_off, nseg, single, kmax, d_out_new, d_count, d_seg_counts, st);
@@ -921,6 +949,8 @@ int rbx_shutdown(rbx_ctx *c) {
         c->pin_small_limit = 0;
         if (c->pin_word) (void)hipHostFree(c->pin_word);
         c->pin_word = nullptr;
+        if (c->pin_tiny) (void)hipHostFree(c->pin_tiny);
+        c->pin_tiny = c->pin_tiny_dev = nullptr;
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->copy_stream = c->stream = nullptr;
@@ -1223,6 +1253,75 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
     return RBX_OK;
 }
 
+// Tiny host batches -- add(T) / contains(T) and collections of up to host_tiny_keys keys and 64 KiB of key
+// bytes: the keys are copied into coherent (uncached, device-mapped) pinned memory, the kernels read them
+// from there over the host link and write their flags back into it, so the call is its launches and one
+// stream sync: no upload, no readback, no zeroed count word.  Counts are the flags' sums on the host
+// (add(Collection) and contains(Collection) both count the keys whose reply is true,
+// M/RedissonBloomFilter.java:104-137,208-236; per segment for the multi-tenant calls).
+static std::atomic<uint64_t> g_tiny_keys{16384};  // rbx_tune("host_tiny_keys"): 0 = off
+static constexpr uint64_t kTinyBytes = 64 << 10;
+// block: flags | segment offsets | key bytes | key offsets (every segment holds a key: nseg <= n)
+static constexpr uint64_t kTinySegAt = kSegMaxKeys, kTinyKeysAt = kTinySegAt + (kSegMaxKeys + 1) * 8;
+static constexpr uint64_t kTinyOffsAt = kTinyKeysAt + kTinyBytes;
+static constexpr size_t kTinyBlock = kTinyOffsAt + (kSegMaxKeys + 1) * 8 + 64;
+
+static bool bloom_tiny_fits(rbx_ctx *c, const rbx_keys *keys) {
+    const uint64_t lim = g_tiny_keys;  // once per call
+    if (!g_small_host || keys->n == 0 || keys->n > lim || keys->n > kSegMaxKeys) return false;
+    const uint64_t nb = keys->offsets ? keys->offsets[keys->n] - keys->offsets[0] : keys->n * keys->stride;
+    if (nb > kTinyBytes) return false;
+    if (c->pin_tiny) return true;
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, kTinyBlock, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return false;
+    }
+    c->pin_tiny = (uint8_t *)h;
+    c->pin_tiny_dev = (uint8_t *)d;
+    return true;
+}
+
+// the keys into the block (the previous call synced before returning); their device view
+static KeysDev tiny_stage(rbx_ctx *c, const rbx_keys *keys) {
+    uint8_t *hp = c->pin_tiny, *dp = c->pin_tiny_dev;
+    const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
+    const uint64_t nb = keys->offsets ? keys->offsets[n] - b0 : n * keys->stride;
+    if (nb) memcpy(hp + kTinyKeysAt, keys->bytes + b0, nb);
+    if (keys->offsets) memcpy(hp + kTinyOffsAt, keys->offsets, (n + 1) * 8);
+    return KeysDev{dp + kTinyKeysAt, keys->offsets ? (const uint64_t *)(dp + kTinyOffsAt) : nullptr, keys->stride, n,
+                   keys->offsets ? b0 : 0};
+}
+
+// after the launches: drain the stream (whatever rc: the block is reused by the next call), then errors
+static int tiny_finish(rbx_ctx *c, int rc) {
+    const hipError_t e = hipGetLastError();
+    const hipError_t es = hipStreamSynchronize(c->stream);
+    RBX_TRY(rc);
+    HIP_TRY(e);
+    HIP_TRY(es);
+    return RBX_OK;
+}
+
+static int bloom_host_tiny(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
+                           uint64_t *out_count, bool is_add) {
+    const KeysDev dk = tiny_stage(c, keys);
+    uint8_t *d_flags = c->pin_tiny_dev;
+    RBX_TRY(tiny_finish(c, is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_flags, nullptr, nullptr, c->stream)
+                                  : run_contains(c, dk, f, d_flags, nullptr, c->stream)));
+    const uint8_t *fl = c->pin_tiny;
+    uint64_t cnt = 0;
+    for (uint64_t i = 0; i < keys->n; ++i) cnt += fl[i];
+    if (out_flags) memcpy(out_flags, fl, keys->n);
+    if (out_count) *out_count = is_add ? (uint64_t)(int64_t)(int32_t)cnt : cnt;  // add(): `int c`
+    return RBX_OK;
+}
+
 static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint32_t k, const rbx_keys *keys,
                          uint8_t *out_flags, uint64_t *out_count, bool is_add) {
     RBX_TRY(validate_keys(keys));
@@ -1257,6 +1356,7 @@ static int bloom_host_op(rbx_ctx *c, const std::string &name, int64_t size, uint
         return RBX_OK;
     }
     FilterDesc f = desc_of(*bm, size_bits(size), k, 0);
+    if (bloom_tiny_fits(c, keys)) return bloom_host_tiny(c, f, k, keys, out_flags, out_count, is_add);
     if (bloom_small_fits(c, keys)) return bloom_host_small(c, f, k, keys, out_flags, out_count, is_add);
     RBX_TRY(c->counters.reserve(64));
     auto *d_count = c->counters.as<unsigned long long>();
@@ -2013,6 +2113,33 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
     ScratchOrder so_(c, c->stream);
     uint64_t mx = 0;  // the largest segment: the per-segment add then skips the chunked path's launches
     for (uint32_t q = 0; q < nseg; ++q) mx = std::max<uint64_t>(mx, seg_offsets[q + 1] - seg_offsets[q]);
+    if (bloom_tiny_fits(c, keys)) {
+        // keys, segment offsets and flags in coherent pinned memory (bloom_host_tiny); the per-segment counts
+        // are the flags' sums (every segment holds a key, so nseg <= n fits the block)
+        const KeysDev dk = tiny_stage(c, keys);
+        memcpy(c->pin_tiny + kTinySegAt, seg_offsets, (uint64_t)(nseg + 1) * 8);
+        const auto *d_seg = (const uint64_t *)(c->pin_tiny_dev + kTinySegAt);
+        uint8_t *d_flags = c->pin_tiny_dev;
+        rbx_keys kd{dk.bytes - dk.off_base, dk.offsets, dk.stride, dk.n};  // the *_dev ABI has no off_base
+        int rc;
+        if (is_add) {
+            c->madd_maxseg_hint = mx;
+            rc = rbx_bloom_add_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
+            c->madd_maxseg_hint = ~0ULL;
+        } else {
+            rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
+        }
+        RBX_TRY(tiny_finish(c, rc));
+        const uint8_t *fl = c->pin_tiny;
+        if (out_counts)
+            for (uint32_t q = 0; q < nseg; ++q) {
+                uint64_t t = 0;
+                for (uint64_t i = seg_offsets[q]; i < seg_offsets[q + 1]; ++i) t += fl[i];
+                out_counts[q] = t;
+            }
+        if (out_flags) memcpy(out_flags, fl, keys->n);
+        return RBX_OK;
+    }
     if ((uint64_t)nseg * 16 + 8 <= kSmallHead && bloom_small_fits(c, keys)) {
         // one transfer: the zeroed per-segment counts, the segment offsets, the keys (bloom_host_small)
         SmallStage sm;
@@ -3535,6 +3662,16 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "host_small_bytes")) {
         if (value < 4096 || value > (64 << 20)) return fail(RBX_E_ILLEGAL_ARGUMENT, "host_small_bytes in [4 KiB, 64 MiB]");
         g_small_bytes = (uint64_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_single_seg_keys")) {
+        if (value < 0 || value > (int64_t)kSegMaxKeys) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_single_seg_keys in [0, 16384]");
+        g_seg_single_keys = (uint64_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "host_tiny_keys")) {
+        if (value < 0 || value > (int64_t)kSegMaxKeys) return fail(RBX_E_ILLEGAL_ARGUMENT, "host_tiny_keys in [0, 16384]");
+        g_tiny_keys = (uint64_t)value;
         return RBX_OK;
     }
     if (!strcmp(key, "host_small_batches")) {

@@ -225,6 +225,9 @@ struct MaddSegArgs {
     uint8_t *out_new;
     unsigned long long *seg_counts;
     uint32_t *big;            // zeroed before the launch
+    // filt == nullptr: one filter passed by value and one segment, all of `keys` (seg_off unused; the
+    // small single-filter adds of run_add and bloom_host_tiny, keys.n <= segmax)
+    FilterDesc single;
 };
 void launch_madd_seg(const MaddSegArgs &a, int klen_fast, hipStream_t st);
 // entries of the 8-byte stream table for a chunk of nadds adds (load <= 8/9 even if every bit is 0)

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_madd_seg(KeysDev keys, const FilterDesc
                                                     const uint64_t *__restrict__ seg_off, uint32_t nseg, uint32_t lgs,
                                                     uint32_t tile, uint64_t segmax, uint8_t *__restrict__ out_new,
                                                     unsigned long long *__restrict__ seg_counts,
-                                                    uint32_t *__restrict__ big) {
+                                                    uint32_t *__restrict__ big, FilterDesc single) {
     extern __shared__ unsigned long long s_dyn[];
     const uint32_t S = 1u << lgs, smask = S - 1u;
     unsigned long long *BT = s_dyn;              // bit << 32 | smallest position in the segment; ~0 empty
@@ -40,13 +40,13 @@ __global__ __launch_bounds__(256) void k_madd_seg(KeysDev keys, const FilterDesc
     __shared__ uint32_t s_red[8];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint32_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
-        const uint64_t a = seg_off[sg], b = seg_off[sg + 1];
+        const uint64_t a = filt ? seg_off[sg] : 0, b = filt ? seg_off[sg + 1] : keys.n;
         if (b - a > segmax) {  // uniform: left to the chunked path
-            if (tid == 0) atomicOr(big, 1u);
+            if (tid == 0 && big) atomicOr(big, 1u);
             continue;
         }
         if (b == a) continue;
-        const FilterDesc f = filt[sg];
+        const FilterDesc f = filt ? filt[sg] : single;
         uint32_t maxidx = 0, nnew = 0;
         uint64_t h1 = 0, h2 = 0;  // the key's hash, computed before the previous tile's store wait
         if (tid < tile && a + tid < b) hash_key<KLEN>(keys, a + tid, h1, h2);
@@ -158,8 +158,9 @@ template <int KLEN, int KMAX>
 static void launch_madd_seg_km(const MaddSegArgs &a, hipStream_t st) {
     const uint32_t lgs = 12;  // 2^12 slots per table, 16 B each: 64 KiB of LDS, two workgroups per CU
     const uint32_t tile = std::min<uint32_t>(256, (5u << (lgs - 3)) / std::max<uint32_t>(a.kmax, 1));  // <= 0.625 load
-    hipLaunchKernelGGL((k_madd_seg<KLEN, KMAX>), dim3(std::min<uint32_t>(a.nseg, a.grid)), dim3(256), (size_t)16 << lgs, st,
-                       a.keys, a.filt, a.seg_off, a.nseg, lgs, tile, a.segmax, a.out_new, a.seg_counts, a.big);
+    hipLaunchKernelGGL((k_madd_seg<KLEN, KMAX>), dim3(a.filt ? std::min<uint32_t>(a.nseg, a.grid) : 1u), dim3(256), (size_t)16 << lgs, st,
+                       a.keys, a.filt, a.seg_off, a.filt ? a.nseg : 1u, lgs, tile, a.segmax, a.out_new, a.seg_counts, a.big,
+                       a.single);
 }
 
 template <int KLEN>

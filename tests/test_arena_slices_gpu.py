@@ -24,17 +24,19 @@ def _sliced(keys, rng):
     return a
 
 
-@pytest.mark.parametrize("small", [1, 0])
+@pytest.mark.parametrize("small", [2, 1, 0])  # 2: the tiny path (coherent pinned keys), 1: one transfer, 0: pipelined
 def test_sliced_arena_bloom_and_hll(client, fresh, small):
     rng = np.random.default_rng(0x511CE + small)
-    keys = [rng.bytes(int(x)) for x in rng.integers(0, 70, size=3000)]
-    assert L.lib().rbx_tune(b"host_small_batches", small) == 0
+    keys = [rng.bytes(int(x)) for x in rng.integers(0, 70, size=1500 if small == 2 else 3000)]  # tiny: <= 64 KiB
+    assert L.lib().rbx_tune(b"host_small_batches", min(small, 1)) == 0
+    assert L.lib().rbx_tune(b"host_tiny_keys", 16384 if small == 2 else 0) == 0
+    na = len(keys) * 2 // 3
     try:
         f = client.getBloomFilter(fresh)
         f.tryInit(50_000, 0.01)
         ref = O.OracleBloom(f.getSize(), f.getHashIterations())
-        cg, ng = f.addEach(_sliced(keys[:2000], rng))
-        cr, nr = ref.add(*O.arena(keys[:2000]), per_key=True)
+        cg, ng = f.addEach(_sliced(keys[:na], rng))
+        cr, nr = ref.add(*O.arena(keys[:na]), per_key=True)
         assert cg == cr and np.array_equal(ng, nr)
         cg, pg = f.containsEach(_sliced(keys, rng))
         cr, pr = ref.contains(*O.arena(keys), per_key=True)
@@ -49,6 +51,7 @@ def test_sliced_arena_bloom_and_hll(client, fresh, small):
         h.delete()
     finally:
         L.lib().rbx_tune(b"host_small_batches", 1)
+        L.lib().rbx_tune(b"host_tiny_keys", 16384)
 
 
 def test_sliced_arena_multi_tenant_and_stream(client, fresh):

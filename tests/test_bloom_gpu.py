@@ -295,13 +295,16 @@ def test_export_import_roundtrip(client, fresh):
     g.delete()
 
 
-@pytest.mark.parametrize("small", [1, 0])
-def test_multi_tenant_parity(client, fresh, small):
-    """Multi-tenant add/contains from a host arena (segments in order, a tenant repeated), per key vs the
-    oracle; small 1: the one-transfer staging (counts, segment offsets and keys in one upload), 0: the
-    separate uploads."""
+@pytest.mark.parametrize("order", [[0, 1, 2, 3, 4, 5, 6, 3, 0], [6, 5, 3, 2, 1, 0]])
+@pytest.mark.parametrize("small", [2, 1, 0])
+def test_multi_tenant_parity(client, fresh, small, order):
+    """Multi-tenant add/contains from a host arena (segments in order; a tenant repeated, or every filter
+    once with k <= 16: the per-segment add), per key vs the oracle; small 2: keys, segment offsets and
+    flags in coherent pinned memory (r06 tiny path, counts from the flags), 1: the one-transfer staging
+    (counts, segment offsets and keys in one upload), 0: the separate uploads."""
     rng = np.random.default_rng(12)
-    assert L.lib().rbx_tune(b"host_small_batches", small) == 0
+    assert L.lib().rbx_tune(b"host_small_batches", min(small, 1)) == 0
+    assert L.lib().rbx_tune(b"host_tiny_keys", 16384 if small == 2 else 0) == 0
     names = [f"{fresh}-{t}" for t in range(7)]
     shapes = [(14377587, 10), (729, 5), (9585, 7), (64, 7), (1000, 40), (1 << 20, 3), (100003, 17)]
     refs = []
@@ -310,7 +313,6 @@ def test_multi_tenant_parity(client, fresh, small):
         refs.append(O.OracleBloom(m, k))
     handles = [BloomHandle(client, n) for n in names]
     # segments: tenant order with a repeated tenant (sequential semantics across segments)
-    order = [0, 1, 2, 3, 4, 5, 6, 3, 0]
     sizes = [int(x) for x in rng.integers(1, 400, size=len(order))]
     keys, segs = [], [0]
     for t, sz in zip(order, sizes):
@@ -326,6 +328,7 @@ def test_multi_tenant_parity(client, fresh, small):
         assert np.array_equal(flags[int(segs[s]):int(segs[s + 1])], fl)
     probes_c, probes_f = bloom_contains_multi(client, [handles[t] for t in order], segs, Arena(keys), per_key=True)
     L.lib().rbx_tune(b"host_small_batches", 1)
+    L.lib().rbx_tune(b"host_tiny_keys", 16384)
     for s, t in enumerate(order):
         sub = keys[int(segs[s]):int(segs[s + 1])]
         c, fl = refs[t].contains(*O.arena(sub), per_key=True)
@@ -1015,6 +1018,52 @@ def test_host_small_batches(client, fresh, small):
     finally:
         L_.lib().rbx_tune(b"host_small_batches", 1)
         L_.lib().rbx_tune(b"host_small_bytes", 4 << 20)
+    assert f.exportBitmap() == ref.redis_string()
+    assert f.count() == ref.count()
+    f.delete()
+
+
+@pytest.mark.parametrize("tiny,seg", [(16384, 256), (16384, 16384), (0, 256), (0, 0)])
+@pytest.mark.parametrize("k_fpp", [(100_000, 0.01), (10_000, 1e-6)])  # k = 7 and k = 20 (adds past k = 16 fall back)
+def test_host_tiny_batches(client, fresh, tiny, seg, k_fpp):
+    """r06: host batches of <= host_tiny_keys keys and <= 64 KiB of key bytes run from coherent pinned memory
+    (bloom_host_tiny: the kernel reads the keys over the host link and writes the flags back), and
+    single-filter adds of <= add_single_seg_keys keys run the per-segment kernel on one segment; each on and
+    off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
+    (= 64 KiB) / 4,097 keys, 16,384 short keys, variable-length and empty keys -- per-key flags and counts,
+    then the bitmap and the Redis string length, vs the oracle."""
+    from redisson_amd import _lib as L_
+
+    rng = np.random.default_rng(0x7171 + tiny + k_fpp[0])
+    f = client.getBloomFilter(fresh)
+    f.tryInit(*k_fpp)
+    ref = O.OracleBloom(f.getSize(), f.getHashIterations())
+    dup = rng.integers(0, 256, size=(64, 16), dtype=np.uint8)
+    dup[40] = dup[3]
+    dup[63] = dup[3]
+    mats = [rng.integers(0, 256, size=(n, 16), dtype=np.uint8) for n in (1, 255, 256, 4096, 4097)] + [dup] + \
+           [rng.integers(0, 256, size=(16384, 4), dtype=np.uint8)]
+    var = [[rng.bytes(int(x)) for x in rng.integers(0, 91, size=300)], [b""] * 5,
+           [b"k-%d" % (i % 7) for i in range(50)]]  # repeats inside the batch
+    batches = [(Arena.fixed(m), O.fixed_arena(m)) for m in mats] + [(Arena(v), O.arena(v)) for v in var]
+    assert L_.lib().rbx_tune(b"host_tiny_keys", tiny) == 0
+    assert L_.lib().rbx_tune(b"add_single_seg_keys", seg) == 0
+    try:
+        for a, o in batches:
+            cg, pg = f.containsEach(a)
+            cr, pr = ref.contains(*o, per_key=True)
+            assert cg == cr and np.array_equal(pg, pr)
+            cg, ng = f.addEach(a)
+            cr, nr = ref.add(*o, per_key=True)
+            assert cg == cr and np.array_equal(ng, nr)
+            assert f.add(a) == ref.add(*o)  # again: nothing new, count only
+            assert f.contains(a) == ref.contains(*o)
+        for key in (bytes(mats[3][9]), b"never-added-key"):  # add(T) / contains(T)
+            assert f.contains(Arena([key])) == ref.contains(*O.arena([key]))
+            assert f.add(Arena([key])) == ref.add(*O.arena([key]))
+    finally:
+        L_.lib().rbx_tune(b"host_tiny_keys", 16384)
+        L_.lib().rbx_tune(b"add_single_seg_keys", 256)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()

@@ -75,6 +75,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="*", default=["gather", "stage1", "sizes", "add"])
     ap.add_argument("--keys", type=int, default=100_000_000)
+    ap.add_argument("--tiny-keys", type=int, default=16384)  # smallbatch: host_tiny_keys
+    ap.add_argument("--seg-keys", type=int, default=256)  # smallbatch: add_single_seg_keys
     a = ap.parse_args()
     for kv in filter(None, os.environ.get("RBX_TUNE", "").split(",")):  # process-wide rbx_tune settings
         key, val = kv.split("=")
@@ -287,19 +289,34 @@ def main():
         torch.cuda.synchronize()
         rng = np.random.default_rng(5)
         hostkeys = base[:65536].cpu().numpy()
-        fresh = torch.randint(0, 256, (300 * 4096, 16), dtype=torch.uint8, device="cuda", generator=g)
-        for nb in [1, 16, 256, 4096, 65536]:
+        fresh = torch.randint(0, 256, (2 * 320 * 4096, 16), dtype=torch.uint8, device="cuda", generator=g)
+        tiny_keys, seg_keys = a.tiny_keys, a.seg_keys
+        assert L.lib().rbx_tune(b"host_tiny_keys", tiny_keys) == 0
+        assert L.lib().rbx_tune(b"add_single_seg_keys", seg_keys) == 0
+        for nb in [1, 16, 256, 1024, 4096, 65536]:
             res = {}
             present = Arena.fixed(hostkeys[:nb])
             adds = [Arena.fixed(rng.integers(0, 256, size=(nb, 16), dtype=np.uint8)) for _ in range(20)]
+            # adds of new keys: every call (warmup and timed, and every variant below) its own keys
+            hpool = rng.integers(0, 256, size=(3 * 320 * nb, 16), dtype=np.uint8) if nb <= 4096 else None
+
+            def add_host_new(v):
+                ars = [Arena.fixed(hpool[(v * 320 + j) * nb:(v * 320 + j + 1) * nb]) for j in range(320)]
+                return lambda i: fb.add(ars[i])
+
+            def add_dev_new(v):
+                return lambda i: (h.add_dev(device_keys(fresh.data_ptr() + 16 * (v * 320 + i) * min(nb, 4096), nb, 16),
+                                            cnt.data_ptr(), stream=sp), stream.synchronize())
+
             calls = {
                 "contains_host": lambda i: fb.contains(present),
-                "add_host": lambda i: fb.add(adds[i % 20]),
+                "add_host": lambda i: fb.add(adds[i % 20]),  # re-adds: 20 batches in turn
                 "contains_dev": lambda i: (h.contains_dev(device_keys(base.data_ptr(), nb, 16), cnt.data_ptr() + 8,
                                                           stream=sp), stream.synchronize()),
-                "add_dev": lambda i: (h.add_dev(device_keys(fresh.data_ptr() + 16 * ((i * nb) % (fresh.shape[0] - nb)),
-                                                            nb, 16), cnt.data_ptr(), stream=sp), stream.synchronize()),
             }
+            if nb <= 4096:
+                calls["add_host_new"] = add_host_new(0)
+                calls["add_dev_new"] = add_dev_new(0)
             if nb == 1:
                 calls["contains_one_object"] = lambda i: fb.contains(bytes(hostkeys[0]))
             if nb >= 4 and nb <= 4096:  # one multi-tenant host call over 4 filters (an RBatch of 4 collections)
@@ -320,11 +337,33 @@ def main():
                 calls["pfadd_sparse_host"] = lambda i: client.getHyperLogLog(f"sb-hs-{nb}-{i // 20}").addAll(
                     adds[i % 20])
                 calls["pfcount_dense_host"] = lambda i: hd.count()
+            # the tiny path (bloom_host_tiny, <= host_tiny_keys keys) and the one-segment add
+            # (add_single_seg_keys) against the r05 paths
+            def off(fn, *knobs):
+                def g(i):
+                    for kb in knobs:
+                        L.lib().rbx_tune(kb, 0)
+                    try:
+                        return fn(i)
+                    finally:
+                        L.lib().rbx_tune(b"host_tiny_keys", tiny_keys)
+                        L.lib().rbx_tune(b"add_single_seg_keys", seg_keys)
+                return g
+
+            if nb <= 16384:
+                calls["contains_host_tiny_off"] = off(calls["contains_host"], b"host_tiny_keys")
+                calls["add_host_tiny_off"] = off(calls["add_host"], b"host_tiny_keys")
+                calls["add_host_seg_off"] = off(calls["add_host"], b"add_single_seg_keys")
+                calls["add_host_r05"] = off(calls["add_host"], b"host_tiny_keys", b"add_single_seg_keys")
+            if nb <= 4096:
+                calls["add_host_new_seg_off"] = off(add_host_new(1), b"add_single_seg_keys")
+                calls["add_host_new_r05"] = off(add_host_new(2), b"host_tiny_keys", b"add_single_seg_keys")
+                calls["add_dev_new_seg_off"] = off(add_dev_new(1), b"add_single_seg_keys")
             for kind, fn in calls.items():
                 for i in range(20):
                     fn(i)
                 ts = []
-                for i in range(300):
+                for i in range(20, 320):
                     t0 = time.perf_counter()
                     fn(i)
                     ts.append(time.perf_counter() - t0)
