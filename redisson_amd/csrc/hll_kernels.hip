@@ -90,7 +90,9 @@ __global__ __launch_bounds__(kPfaddThreads) void k_hll_pfadd(KeysDev elems, cons
         }
     }
     any = __syncthreads_or(any);
-    if (threadIdx.x == 0 && any) atomicOr(&changed[tile.seg], 1u);
+    // every writer stores 1 into a zeroed word: a plain (atomic) store, not an RMW -- the word may sit in
+    // coherent host memory (bloom_host_tiny), where a device RMW would be a host-link atomic
+    if (threadIdx.x == 0 && any) __hip_atomic_store(&changed[tile.seg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void launch_hll_pfadd(const KeysDev &elems, int elen_fast, const HllSeg *d_tiles, uint32_t ntiles,

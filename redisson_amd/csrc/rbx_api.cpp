@@ -1264,7 +1264,23 @@ static constexpr uint64_t kTinyBytes = 64 << 10;
 // block: flags | segment offsets | key bytes | key offsets (every segment holds a key: nseg <= n)
 static constexpr uint64_t kTinySegAt = kSegMaxKeys, kTinyKeysAt = kTinySegAt + (kSegMaxKeys + 1) * 8;
 static constexpr uint64_t kTinyOffsAt = kTinyKeysAt + kTinyBytes;
-static constexpr size_t kTinyBlock = kTinyOffsAt + (kSegMaxKeys + 1) * 8 + 64;
+// then the small tables a call would upload (PFADD's tile list and sparse-replay items: TinyArena)
+static constexpr uint64_t kTinyArenaAt = kTinyOffsAt + (kSegMaxKeys + 1) * 8 + 64, kTinyArenaBytes = 64 << 10;
+static constexpr size_t kTinyBlock = kTinyArenaAt + kTinyArenaBytes;
+
+// bump allocation in the block's arena region: the device view of a copy of src, nullptr when full (the
+// caller then uploads as usual).  Every copy stays put until the call's final sync.
+struct TinyArena {
+    uint8_t *h, *d;
+    size_t cap, used;
+    const void *put(const void *src, size_t n) {
+        const size_t at = (used + 63) / 64 * 64;
+        if (at + n > cap) return nullptr;
+        memcpy(h + at, src, n);
+        used = at + n;
+        return d + at;
+    }
+};
 
 static bool bloom_tiny_fits(rbx_ctx *c, const rbx_keys *keys) {
     const uint64_t lim = g_tiny_keys;  // once per call
@@ -2261,8 +2277,14 @@ static int hll_bind(rbx_ctx *c, rbx_hll *h, bool create, hipStream_t st) {
 // k_hll_sparse_replay applies each command's updates, in order, to the sparse HLLs' strings on
 // the device (the registers are updated by the PFADD / merge kernels as for dense keys) and sets
 // the sticky promotion word at the first promotion.  `items` = one per sparse HLL of a round.
-static int replay_sparse(rbx_ctx *c, std::vector<HllReplay> &items, const KeysDev &dk, int fl, hipStream_t st) {
+static int replay_sparse(rbx_ctx *c, std::vector<HllReplay> &items, const KeysDev &dk, int fl, hipStream_t st,
+                         TinyArena *ta = nullptr) {
     if (items.empty()) return RBX_OK;
+    if (const void *d = ta ? ta->put(items.data(), items.size() * sizeof(HllReplay)) : nullptr) {  // tiny call
+        launch_hll_sparse_replay(dk, fl, (const HllReplay *)d, (uint32_t)items.size(), kHllSparseMaxBytes, st);
+        HIP_TRY(hipGetLastError());
+        return RBX_OK;
+    }
     const bool same = c->check_cache.size() == items.size() &&
                       memcmp(c->check_cache.data(), items.data(), items.size() * sizeof(HllReplay)) == 0;
     if (!same) {
@@ -2301,7 +2323,7 @@ static int resolve_dense(rbx_ctx *c, HllState *h) {
 // PFADD batch: device elements, commands in order.  Commands naming the same HLL are
 // split into successive launches so each reply sees the previous commands' effect.
 static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64_t *h_seg, const KeysDev &dk,
-                     uint32_t *d_changed, hipStream_t st) {
+                     uint32_t *d_changed, hipStream_t st, TinyArena *ta = nullptr) {
     const uint32_t nseg = (uint32_t)hl.size();
     std::vector<HllSeg> tiles;
     uint32_t s0 = 0;
@@ -2317,26 +2339,31 @@ static int pfadd_run(rbx_ctx *c, const std::vector<HllState *> &hl, const uint64
                 tiles.push_back(HllSeg{hl[s]->d_regs, b, std::min(h_seg[s + 1], b + kTileElems), s, 0});
         }
         if (!tiles.empty()) {
-            // the tile table is cached by content (a steady PFADD pipeline re-sends the same one)
-            const bool single_round = s0 == 0 && s1 == nseg;
-            const bool same = single_round && c->tiles_valid && c->tile_cache.size() == tiles.size() &&
-                              memcmp(c->tile_cache.data(), tiles.data(), tiles.size() * sizeof(HllSeg)) == 0;
-            if (!same) {
-                RBX_TRY(c->hll_tiles.reserve(tiles.size() * sizeof(HllSeg)));
-                // pageable source: staged by the runtime before the call returns; stream order
-                // keeps the previous round's kernel ahead of this overwrite
-                HIP_TRY(hipMemcpyAsync(c->hll_tiles.p, tiles.data(), tiles.size() * sizeof(HllSeg), hipMemcpyHostToDevice, st));
-                c->tiles_valid = single_round;
-                if (single_round) c->tile_cache = tiles;
+            // a tiny call's tile list is read from the coherent block (each round its own copy)
+            const HllSeg *d_tiles = ta ? (const HllSeg *)ta->put(tiles.data(), tiles.size() * sizeof(HllSeg)) : nullptr;
+            if (!d_tiles) {
+                // the tile table is cached by content (a steady PFADD pipeline re-sends the same one)
+                const bool single_round = s0 == 0 && s1 == nseg;
+                const bool same = single_round && c->tiles_valid && c->tile_cache.size() == tiles.size() &&
+                                  memcmp(c->tile_cache.data(), tiles.data(), tiles.size() * sizeof(HllSeg)) == 0;
+                if (!same) {
+                    RBX_TRY(c->hll_tiles.reserve(tiles.size() * sizeof(HllSeg)));
+                    // pageable source: staged by the runtime before the call returns; stream order
+                    // keeps the previous round's kernel ahead of this overwrite
+                    HIP_TRY(hipMemcpyAsync(c->hll_tiles.p, tiles.data(), tiles.size() * sizeof(HllSeg), hipMemcpyHostToDevice, st));
+                    c->tiles_valid = single_round;
+                    if (single_round) c->tile_cache = tiles;
+                }
+                d_tiles = c->hll_tiles.as<HllSeg>();
             }
-            launch_hll_pfadd(dk, fl, c->hll_tiles.as<HllSeg>(), (uint32_t)tiles.size(), d_changed, st);
+            launch_hll_pfadd(dk, fl, d_tiles, (uint32_t)tiles.size(), d_changed, st);
             HIP_TRY(hipGetLastError());
             std::vector<HllReplay> items;  // the round's HLLs are distinct
             for (uint32_t s = s0; s < s1; ++s)
                 if (!hl[s]->dense && h_seg[s + 1] > h_seg[s])
                     items.push_back(HllReplay{hl[s]->d_sp_ops, hl[s]->d_promoted, nullptr, h_seg[s], h_seg[s + 1],
                                               hl[s]->d_regs});
-            RBX_TRY(replay_sparse(c, items, dk, fl, st));
+            RBX_TRY(replay_sparse(c, items, dk, fl, st, ta));
         }
         s0 = s1;
     }
@@ -2365,6 +2392,21 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         created[s] = cr;
     }
     std::vector<uint32_t> ch(nseg);
+    if (nseg <= kSegMaxKeys && bloom_tiny_fits(c, elements)) {
+        // elements, changed words, tile list and replay items in coherent pinned memory (bloom_host_tiny)
+        auto *ch_h = (uint32_t *)(c->pin_tiny + kTinySegAt);
+        memset(ch_h, 0, (size_t)nseg * 4);
+        const KeysDev dk = tiny_stage(c, elements);
+        TinyArena ta{c->pin_tiny + kTinyArenaAt, c->pin_tiny_dev + kTinyArenaAt, kTinyArenaBytes, 0};
+        RBX_TRY(tiny_finish(c, pfadd_run(c, hl, seg_offsets, dk, (uint32_t *)(c->pin_tiny_dev + kTinySegAt), c->stream,
+                                         &ta)));
+        memcpy(ch.data(), ch_h, (size_t)nseg * 4);
+        for (uint32_t s = 0; s < nseg; ++s) {
+            if (ch[s]) hl[s]->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
+            if (out_changed) out_changed[s] = ch[s] || created[s];
+        }
+        return RBX_OK;
+    }
     if (nseg <= kSmallHead / 4 && bloom_small_fits(c, elements)) {
         // one transfer for the elements and the zeroed changed words, one readback (bloom_host_small)
         SmallStage sm;
