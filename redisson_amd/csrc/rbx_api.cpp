@@ -1262,10 +1262,12 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
 static std::atomic<uint64_t> g_tiny_keys{16384};  // rbx_tune("host_tiny_keys"): 0 = off
 static constexpr uint64_t kTinyBytes = 64 << 10;
 // block: flags | segment offsets | key bytes | key offsets (every segment holds a key: nseg <= n)
-static constexpr uint64_t kTinySegAt = kSegMaxKeys, kTinyKeysAt = kTinySegAt + (kSegMaxKeys + 1) * 8;
+// (regions 64-byte aligned: 16-byte keys at a 16-byte boundary take the kernels' fixed-length loads, fast_len)
+static constexpr uint64_t kTinySegAt = kSegMaxKeys, kTinyKeysAt = kTinySegAt + (kSegMaxKeys + 8) * 8;
 static constexpr uint64_t kTinyOffsAt = kTinyKeysAt + kTinyBytes;
 // then the small tables a call would upload (PFADD's tile list and sparse-replay items: TinyArena)
-static constexpr uint64_t kTinyArenaAt = kTinyOffsAt + (kSegMaxKeys + 1) * 8 + 64, kTinyArenaBytes = 64 << 10;
+static constexpr uint64_t kTinyArenaAt = kTinyOffsAt + (kSegMaxKeys + 8) * 8, kTinyArenaBytes = 64 << 10;
+static_assert(kTinyKeysAt % 64 == 0 && kTinyOffsAt % 64 == 0 && kTinyArenaAt % 64 == 0, "aligned regions");
 static constexpr size_t kTinyBlock = kTinyArenaAt + kTinyArenaBytes;
 
 // bump allocation in the block's arena region: the device view of a copy of src, nullptr when full (the

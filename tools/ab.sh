@@ -9,7 +9,7 @@ for i in $(seq "$N"); do
   for lib in "$OLD" "$R/redisson_amd/librbx.so"; do
     RBX_LIB_PATH=$lib timeout -k 10 240 python3 "$R/bench.py" --workload "$W" --steps 10 --warmup 2 --no-cpu-baseline --no-hostpath --legs none \
       > "$R/gpurun_out/ab_run.log" 2>&1 || exit 1
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(json.dumps({'lib': sys.argv[2], 'ms_per_step': d['ms_per_step'], 'value': d['value'], 'add_ms': d.get('extra', {}).get('add_ms')}))" \
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(json.dumps({'lib': sys.argv[2], 'ms_per_step': d['ms_per_step'], 'value': d['value'], 'add_ms': (d.get('add') or {}).get('ms_per_step')}))" \
       "$R/gpurun_out/ab_run.log" "$lib" >> "$R/gpurun_out/ab_$W.jsonl" || exit 1
   done
 done
