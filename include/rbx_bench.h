@@ -96,6 +96,8 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *   "add_single_seg_keys"   single-filter adds of at most this many keys with k <= 16 (0..16384,
  *                           default 256) run the per-segment kernel on one segment (one launch, first
  *                           setters in LDS) instead of the table path; 0: the table path
+ *   "add_one_key"           1 (default): a one-key single-filter add with k <= 16 takes
+ *                           k_bloom_add_one (one lane, no first-setter table); 0: as above
  * Profiling build only (librbx_diag.so, `make diag`; librbx.so rejects them): "stream_diag",
  * "contains_partition_flags", "add_partition_diag" -- timing diagnostics that make answers wrong
  * (rbx_kernels.h kDiag).  Removed in r06 with the variants they selected (measured slower, never

@@ -796,6 +796,61 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
     }
 }
 
+// add(T) (M/RedissonBloomFilter.java:99-102): SETBIT of the key's k bits, new iff one of them was 0.  One
+// key has no earlier key of its batch to lose a bit to, so it needs no first-setter table: one lane reads
+// the Redis length and the k words, ORs every zero bit in (non-returning atomics), writes the reply and
+// raises the length.  The context's call order keeps every other writer of the bitmap out meanwhile.
+// (A 1-key call through the one-segment kernel spends ~10 us on the GPU, through this one ~5 us.)
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(64) void k_bloom_add_one(KeysDev keys, FilterDesc f, uint8_t *__restrict__ out,
+                                                      unsigned long long *__restrict__ count) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long len0 = __hip_atomic_load(f.redis_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t h1, h2;
+    hash_key<KLEN>(keys, 0, h1, h2);
+    uint32_t idxs[KMAX], word[KMAX], maxidx = 0;
+    uint64_t h = h1;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if ((uint32_t)j < f.k) {
+            const uint32_t idx = mod63(h & 0x7fffffffffffffffULL, f.mp);
+            idxs[j] = idx;
+            word[j] = f.bm[idx >> 5];
+            maxidx = idx > maxidx ? idx : maxidx;
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    bool isnew = false;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if ((uint32_t)j < f.k && (word[j] & bit_in_word(idxs[j])) == 0u) {
+            isnew = true;
+            atomicOr(&f.bm[idxs[j] >> 5], bit_in_word(idxs[j]));
+        }
+    }
+    if (out) out[0] = isnew;
+    if (count && isnew) atomicAdd(count, 1ULL);
+    const unsigned long long len = (unsigned long long)(maxidx >> 3) + 1ULL;  // every SETBIT grows the string
+    if (len > len0) atomicMax(f.redis_len, len);
+}
+
+template <int KLEN>
+static void launch_add_one_len(const KeysDev &keys, const FilterDesc &f, uint8_t *out, unsigned long long *count,
+                               hipStream_t st) {
+    if (f.k <= 8) hipLaunchKernelGGL((k_bloom_add_one<KLEN, 8>), dim3(1), dim3(64), 0, st, keys, f, out, count);
+    else hipLaunchKernelGGL((k_bloom_add_one<KLEN, 16>), dim3(1), dim3(64), 0, st, keys, f, out, count);
+}
+
+void launch_bloom_add_one(const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
+                          unsigned long long *count, hipStream_t st) {
+    switch (klen_fast) {
+    case 16: launch_add_one_len<16>(keys, f, out, count, st); break;
+    case 32: launch_add_one_len<32>(keys, f, out, count, st); break;
+    case 64: launch_add_one_len<64>(keys, f, out, count, st); break;
+    default: launch_add_one_len<0>(keys, f, out, count, st); break;
+    }
+}
+
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st) {
     const unsigned grid = grid_for((nbytes + 15) / 16, kMaxGrid);
     hipLaunchKernelGGL(k_bitcount, dim3(grid), dim3(256), 0, st, bytes, nbytes, out);

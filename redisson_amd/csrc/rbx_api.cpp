@@ -707,6 +707,7 @@ static int run_add_partitioned(rbx_ctx *c, const KeysDev &keys, const FilterDesc
 // commit: one launch.  Its plain word stores need the bitmap to itself, which the context's call order
 // gives (every call waits for the previous one's stream, ScratchOrder).
 static std::atomic<uint64_t> g_seg_single_keys{256};  // rbx_tune("add_single_seg_keys"): 0 = off
+static std::atomic<int> g_add_one{1};  // rbx_tune("add_one_key"): 1 = a 1-key add takes k_bloom_add_one
 
 static bool use_seg_single(const FilterDesc &f, uint64_t n, uint64_t lim) { return f.k <= 16 && n <= lim; }
 
@@ -726,6 +727,11 @@ static int run_add(rbx_ctx *c, const KeysDev &keys, const FilterDesc *d_filt, co
                    uint32_t nseg, const FilterDesc &single, uint32_t kmax, uint8_t *d_out_new,
                    unsigned long long *d_count, unsigned long long *d_seg_counts, hipStream_t st) {
     if (keys.n == 0) return RBX_OK;
+    if (d_filt == nullptr && keys.n == 1 && single.k <= 16 && g_add_one) {
+        launch_bloom_add_one(keys, fast_len(keys), single, d_out_new, d_count, st);
+        HIP_TRY(hipGetLastError());
+        return RBX_OK;
+    }
     if (d_filt == nullptr && use_seg_single(single, keys.n, g_seg_single_keys)) {
         launch_seg_single(keys, single, d_out_new, d_count, st);
         HIP_TRY(hipGetLastError());
@@ -3706,6 +3712,11 @@ int rbx_tune(const char *key, int value) {
     if (!strcmp(key, "host_small_bytes")) {
         if (value < 4096 || value > (64 << 20)) return fail(RBX_E_ILLEGAL_ARGUMENT, "host_small_bytes in [4 KiB, 64 MiB]");
         g_small_bytes = (uint64_t)value;
+        return RBX_OK;
+    }
+    if (!strcmp(key, "add_one_key")) {
+        if (value != 0 && value != 1) return fail(RBX_E_ILLEGAL_ARGUMENT, "add_one_key in {0, 1}");
+        g_add_one = value;
         return RBX_OK;
     }
     if (!strcmp(key, "add_single_seg_keys")) {

@@ -1023,13 +1023,13 @@ def test_host_small_batches(client, fresh, small):
     f.delete()
 
 
-@pytest.mark.parametrize("tiny,seg", [(16384, 256), (16384, 16384), (0, 256), (0, 0)])
+@pytest.mark.parametrize("tiny,seg,one", [(16384, 256, 1), (16384, 256, 0), (16384, 16384, 1), (0, 256, 1), (0, 0, 0)])
 @pytest.mark.parametrize("k_fpp", [(100_000, 0.01), (10_000, 1e-6)])  # k = 7 and k = 20 (adds past k = 16 fall back)
-def test_host_tiny_batches(client, fresh, tiny, seg, k_fpp):
+def test_host_tiny_batches(client, fresh, tiny, seg, one, k_fpp):
     """r06: host batches of <= host_tiny_keys keys and <= 64 KiB of key bytes run from coherent pinned memory
     (bloom_host_tiny: the kernel reads the keys over the host link and writes the flags back), and
-    single-filter adds of <= add_single_seg_keys keys run the per-segment kernel on one segment; each on and
-    off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
+    single-filter adds of <= add_single_seg_keys keys run the per-segment kernel on one segment, and one-key
+    adds k_bloom_add_one (add_one_key); each on and off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
     (= 64 KiB) / 4,097 keys, 16,384 short keys, variable-length and empty keys -- per-key flags and counts,
     then the bitmap and the Redis string length, vs the oracle."""
     from redisson_amd import _lib as L_
@@ -1048,6 +1048,7 @@ def test_host_tiny_batches(client, fresh, tiny, seg, k_fpp):
     batches = [(Arena.fixed(m), O.fixed_arena(m)) for m in mats] + [(Arena(v), O.arena(v)) for v in var]
     assert L_.lib().rbx_tune(b"host_tiny_keys", tiny) == 0
     assert L_.lib().rbx_tune(b"add_single_seg_keys", seg) == 0
+    assert L_.lib().rbx_tune(b"add_one_key", one) == 0
     try:
         for a, o in batches:
             cg, pg = f.containsEach(a)
@@ -1058,12 +1059,13 @@ def test_host_tiny_batches(client, fresh, tiny, seg, k_fpp):
             assert cg == cr and np.array_equal(ng, nr)
             assert f.add(a) == ref.add(*o)  # again: nothing new, count only
             assert f.contains(a) == ref.contains(*o)
-        for key in (bytes(mats[3][9]), b"never-added-key"):  # add(T) / contains(T)
+        for key in [bytes(mats[3][9]), b"never-added-key", b""] + [rng.bytes(int(x)) for x in rng.integers(0, 80, 40)]:
             assert f.contains(Arena([key])) == ref.contains(*O.arena([key]))
             assert f.add(Arena([key])) == ref.add(*O.arena([key]))
     finally:
         L_.lib().rbx_tune(b"host_tiny_keys", 16384)
         L_.lib().rbx_tune(b"add_single_seg_keys", 256)
+        L_.lib().rbx_tune(b"add_one_key", 1)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()

@@ -298,7 +298,7 @@ def main():
             present = Arena.fixed(hostkeys[:nb])
             adds = [Arena.fixed(rng.integers(0, 256, size=(nb, 16), dtype=np.uint8)) for _ in range(20)]
             # adds of new keys: every call (warmup and timed, and every variant below) its own keys
-            hpool = rng.integers(0, 256, size=(3 * 320 * nb, 16), dtype=np.uint8) if nb <= 4096 else None
+            hpool = rng.integers(0, 256, size=(5 * 320 * nb, 16), dtype=np.uint8) if nb <= 4096 else None
 
             def add_host_new(v):
                 ars = [Arena.fixed(hpool[(v * 320 + j) * nb:(v * 320 + j + 1) * nb]) for j in range(320)]
@@ -348,6 +348,7 @@ def main():
                     finally:
                         L.lib().rbx_tune(b"host_tiny_keys", tiny_keys)
                         L.lib().rbx_tune(b"add_single_seg_keys", seg_keys)
+                        L.lib().rbx_tune(b"add_one_key", 1)
                 return g
 
             if nb <= 16384:
@@ -359,6 +360,9 @@ def main():
                 calls["add_host_new_seg_off"] = off(add_host_new(1), b"add_single_seg_keys")
                 calls["add_host_new_r05"] = off(add_host_new(2), b"host_tiny_keys", b"add_single_seg_keys")
                 calls["add_dev_new_seg_off"] = off(add_dev_new(1), b"add_single_seg_keys")
+            if nb == 1:  # the one-segment kernel instead of k_bloom_add_one
+                calls["add_host_new_one_off"] = off(add_host_new(3), b"add_one_key")
+                calls["add_dev_new_one_off"] = off(add_dev_new(3), b"add_one_key")
             for kind, fn in calls.items():
                 for i in range(20):
                     fn(i)
