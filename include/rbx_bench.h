@@ -98,6 +98,9 @@ int rbx_bench_stream_geometry(rbx_ctx *ctx, uint64_t *out);
  *                           setters in LDS) instead of the table path; 0: the table path
  *   "add_one_key"           1 (default): a one-key single-filter add with k <= 16 takes
  *                           k_bloom_add_one (one lane, no first-setter table); 0: as above
+ *   "host_tiny_spin"        1 (default): a one-key host add/contains (k <= 16) spins on its kernel's
+ *                           completion word in the pinned block (2 ms, then a stream sync);
+ *                           0: a stream sync
  * Profiling build only (librbx_diag.so, `make diag`; librbx.so rejects them): "stream_diag",
  * "contains_partition_flags", "add_partition_diag" -- timing diagnostics that make answers wrong
  * (rbx_kernels.h kDiag).  Removed in r06 with the variants they selected (measured slower, never

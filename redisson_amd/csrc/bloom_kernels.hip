@@ -801,9 +801,12 @@ void launch_bloom_add_chunk(const AddChunkArgs &a, int klen_fast, hipStream_t st
 // the Redis length and the k words, ORs every zero bit in (non-returning atomics), writes the reply and
 // raises the length.  The context's call order keeps every other writer of the bitmap out meanwhile.
 // (A 1-key call through the one-segment kernel spends ~10 us on the GPU, through this one ~5 us.)
+// `done` (nullable, coherent host memory): the lane's last store is seq there, after every other access of
+// the call (a system-scope release), so the host can spin on it instead of waiting for the stream (§3.10)
 template <int KLEN, int KMAX>
 __global__ __launch_bounds__(64) void k_bloom_add_one(KeysDev keys, FilterDesc f, uint8_t *__restrict__ out,
-                                                      unsigned long long *__restrict__ count) {
+                                                      unsigned long long *__restrict__ count, uint32_t *done,
+                                                      uint32_t seq) {
     if (threadIdx.x != 0) return;
     const unsigned long long len0 = __hip_atomic_load(f.redis_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t h1, h2;
@@ -832,22 +835,55 @@ __global__ __launch_bounds__(64) void k_bloom_add_one(KeysDev keys, FilterDesc f
     if (count && isnew) atomicAdd(count, 1ULL);
     const unsigned long long len = (unsigned long long)(maxidx >> 3) + 1ULL;  // every SETBIT grows the string
     if (len > len0) atomicMax(f.redis_len, len);
+    if (done) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// contains(T): one key, one lane, every word gathered at once; `done` as in k_bloom_add_one
+template <int KLEN, int KMAX>
+__global__ __launch_bounds__(64) void k_bloom_contains_one(KeysDev keys, const uint32_t *__restrict__ bm, ModParams mp,
+                                                           uint32_t k, uint8_t *__restrict__ out, uint32_t *done,
+                                                           uint32_t seq) {
+    if (threadIdx.x != 0) return;
+    uint64_t h1, h2;
+    hash_key<KLEN>(keys, 0, h1, h2);
+    uint32_t idxs[KMAX], word[KMAX];
+    uint64_t h = h1;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if ((uint32_t)j < k) {
+            idxs[j] = mod63(h & 0x7fffffffffffffffULL, mp);
+            word[j] = bm[idxs[j] >> 5];
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+        if ((uint32_t)j < k) all &= (word[j] & bit_in_word(idxs[j])) != 0u;
+    if (out) out[0] = all;
+    if (done) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int KLEN>
-static void launch_add_one_len(const KeysDev &keys, const FilterDesc &f, uint8_t *out, unsigned long long *count,
-                               hipStream_t st) {
-    if (f.k <= 8) hipLaunchKernelGGL((k_bloom_add_one<KLEN, 8>), dim3(1), dim3(64), 0, st, keys, f, out, count);
-    else hipLaunchKernelGGL((k_bloom_add_one<KLEN, 16>), dim3(1), dim3(64), 0, st, keys, f, out, count);
+static void launch_one_len(bool add, const KeysDev &keys, const FilterDesc &f, uint8_t *out, unsigned long long *count,
+                           uint32_t *done, uint32_t seq, hipStream_t st) {
+    if (add && f.k <= 8)
+        hipLaunchKernelGGL((k_bloom_add_one<KLEN, 8>), dim3(1), dim3(64), 0, st, keys, f, out, count, done, seq);
+    else if (add)
+        hipLaunchKernelGGL((k_bloom_add_one<KLEN, 16>), dim3(1), dim3(64), 0, st, keys, f, out, count, done, seq);
+    else if (f.k <= 8)
+        hipLaunchKernelGGL((k_bloom_contains_one<KLEN, 8>), dim3(1), dim3(64), 0, st, keys, f.bm, f.mp, f.k, out, done, seq);
+    else
+        hipLaunchKernelGGL((k_bloom_contains_one<KLEN, 16>), dim3(1), dim3(64), 0, st, keys, f.bm, f.mp, f.k, out, done, seq);
 }
 
-void launch_bloom_add_one(const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
-                          unsigned long long *count, hipStream_t st) {
+void launch_bloom_one(bool add, const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
+                      unsigned long long *count, uint32_t *done, uint32_t seq, hipStream_t st) {
     switch (klen_fast) {
-    case 16: launch_add_one_len<16>(keys, f, out, count, st); break;
-    case 32: launch_add_one_len<32>(keys, f, out, count, st); break;
-    case 64: launch_add_one_len<64>(keys, f, out, count, st); break;
-    default: launch_add_one_len<0>(keys, f, out, count, st); break;
+    case 16: launch_one_len<16>(add, keys, f, out, count, done, seq, st); break;
+    case 32: launch_one_len<32>(add, keys, f, out, count, done, seq, st); break;
+    case 64: launch_one_len<64>(add, keys, f, out, count, done, seq, st); break;
+    default: launch_one_len<0>(add, keys, f, out, count, done, seq, st); break;
     }
 }
 

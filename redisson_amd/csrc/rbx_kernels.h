@@ -243,9 +243,10 @@ __host__ __device__ inline uint32_t t8_log2(uint32_t nadds, uint32_t kmax) {
 void launch_stream_chunk(const StreamChunkArgs &a, int klen_fast, hipStream_t st);
 void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *bm, const ModParams &mp,
                            uint32_t k, uint8_t *out, unsigned long long *count, hipStream_t st);
-// add(T): one key into one filter (k <= 16), one lane: no first-setter table (run_add, keys.n == 1)
-void launch_bloom_add_one(const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
-                          unsigned long long *count, hipStream_t st);
+// add(T) / contains(T): one key of one filter (k <= 16), one lane; an add needs no first-setter table
+// (run_add, keys.n == 1).  done (nullable): seq is stored there last, at system scope (bloom_host_tiny)
+void launch_bloom_one(bool add, const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
+                      unsigned long long *count, uint32_t *done, uint32_t seq, hipStream_t st);
 // tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)
 void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,

@@ -118,5 +118,6 @@ def test_product_library_has_no_wrong_answer_switches():
     assert lib.rbx_tune(b"add_multi_table8", 1) == -1
     for key, val in ((b"add_multi_table8", 2), (b"contains_stage1", 4), (b"stream_table8", 1),
                      (b"add_multi_seg_grid", 8192), (b"host_small_bytes", 4 << 20), (b"host_tiny_keys", 16384),
-                     (b"add_single_seg_keys", 256), (b"add_one_key", 1)):
+                     (b"add_single_seg_keys", 256), (b"add_one_key", 1),
+                     (b"host_tiny_spin", 1)):
         assert lib.rbx_tune(key, val) == 0, key

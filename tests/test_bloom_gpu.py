@@ -1023,13 +1023,15 @@ def test_host_small_batches(client, fresh, small):
     f.delete()
 
 
-@pytest.mark.parametrize("tiny,seg,one", [(16384, 256, 1), (16384, 256, 0), (16384, 16384, 1), (0, 256, 1), (0, 0, 0)])
-@pytest.mark.parametrize("k_fpp", [(100_000, 0.01), (10_000, 1e-6)])  # k = 7 and k = 20 (adds past k = 16 fall back)
-def test_host_tiny_batches(client, fresh, tiny, seg, one, k_fpp):
+@pytest.mark.parametrize("tiny,seg,one,spin", [(16384, 256, 1, 1), (16384, 256, 1, 0), (16384, 256, 0, 1),
+                                               (16384, 16384, 1, 1), (0, 256, 1, 1), (0, 0, 0, 0)])
+@pytest.mark.parametrize("k_fpp", [(100_000, 0.01), (10_000, 1e-6)])  # k = 7 and k = 20 (past k = 16: fallbacks)
+def test_host_tiny_batches(client, fresh, tiny, seg, one, spin, k_fpp):
     """r06: host batches of <= host_tiny_keys keys and <= 64 KiB of key bytes run from coherent pinned memory
     (bloom_host_tiny: the kernel reads the keys over the host link and writes the flags back), and
     single-filter adds of <= add_single_seg_keys keys run the per-segment kernel on one segment, and one-key
-    adds k_bloom_add_one (add_one_key); each on and off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
+    adds k_bloom_add_one (add_one_key), and one-key host calls spin on the kernel's completion word
+    (host_tiny_spin); each on and off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
     (= 64 KiB) / 4,097 keys, 16,384 short keys, variable-length and empty keys -- per-key flags and counts,
     then the bitmap and the Redis string length, vs the oracle."""
     from redisson_amd import _lib as L_
@@ -1049,6 +1051,7 @@ def test_host_tiny_batches(client, fresh, tiny, seg, one, k_fpp):
     assert L_.lib().rbx_tune(b"host_tiny_keys", tiny) == 0
     assert L_.lib().rbx_tune(b"add_single_seg_keys", seg) == 0
     assert L_.lib().rbx_tune(b"add_one_key", one) == 0
+    assert L_.lib().rbx_tune(b"host_tiny_spin", spin) == 0
     try:
         for a, o in batches:
             cg, pg = f.containsEach(a)
@@ -1066,6 +1069,7 @@ def test_host_tiny_batches(client, fresh, tiny, seg, one, k_fpp):
         L_.lib().rbx_tune(b"host_tiny_keys", 16384)
         L_.lib().rbx_tune(b"add_single_seg_keys", 256)
         L_.lib().rbx_tune(b"add_one_key", 1)
+        L_.lib().rbx_tune(b"host_tiny_spin", 1)
     assert f.exportBitmap() == ref.redis_string()
     assert f.count() == ref.count()
     f.delete()

@@ -349,6 +349,7 @@ def main():
                         L.lib().rbx_tune(b"host_tiny_keys", tiny_keys)
                         L.lib().rbx_tune(b"add_single_seg_keys", seg_keys)
                         L.lib().rbx_tune(b"add_one_key", 1)
+                        L.lib().rbx_tune(b"host_tiny_spin", 1)
                 return g
 
             if nb <= 16384:
@@ -362,6 +363,8 @@ def main():
                 calls["add_dev_new_seg_off"] = off(add_dev_new(1), b"add_single_seg_keys")
             if nb == 1:  # the one-segment kernel instead of k_bloom_add_one
                 calls["add_host_new_one_off"] = off(add_host_new(3), b"add_one_key")
+                calls["add_host_new_spin_off"] = off(add_host_new(4), b"host_tiny_spin")
+                calls["contains_host_spin_off"] = off(calls["contains_host"], b"host_tiny_spin")
                 calls["add_dev_new_one_off"] = off(add_dev_new(3), b"add_one_key")
             for kind, fn in calls.items():
                 for i in range(20):
