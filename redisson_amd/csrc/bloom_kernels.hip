@@ -887,6 +887,16 @@ void launch_bloom_one(bool add, const KeysDev &keys, int klen_fast, const Filter
     }
 }
 
+// the completion word of a tiny host call whose work is several kernels or workgroups: stream order puts it
+// after all of them (bloom_host_tiny; 9.6 vs 11.5 us for a stream sync, tools/syncbench.hip)
+__global__ void k_done_word(uint32_t *done, uint32_t seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_done_word(uint32_t *done, uint32_t seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_done_word, dim3(1), dim3(64), 0, st, done, seq);
+}
+
 void launch_bitcount(const uint8_t *bytes, uint64_t nbytes, unsigned long long *out, hipStream_t st) {
     const unsigned grid = grid_for((nbytes + 15) / 16, kMaxGrid);
     hipLaunchKernelGGL(k_bitcount, dim3(grid), dim3(256), 0, st, bytes, nbytes, out);

@@ -1327,43 +1327,56 @@ static KeysDev tiny_stage(rbx_ctx *c, const rbx_keys *keys) {
                    keys->offsets ? b0 : 0};
 }
 
-// after the launches: drain the stream (whatever rc: the block is reused by the next call), then errors
-static int tiny_finish(rbx_ctx *c, int rc) {
-    const hipError_t e = hipGetLastError();
-    const hipError_t es = hipStreamSynchronize(c->stream);
-    RBX_TRY(rc);
-    HIP_TRY(e);
-    HIP_TRY(es);
-    return RBX_OK;
-}
-
-// A one-key call (add(T) / contains(T), k <= 16) runs one lane whose last store is a sequence number in the
-// block; the host spins on it (`host_tiny_spin`, default 1) instead of waiting for the stream: 7.2 vs 11.5 us
-// for a one-wave kernel (tools/syncbench.hip).  After 2 ms without it (a queue still busy with earlier work,
-// or a fault) it waits for the stream, which also reports any error.
+// A tiny call learns that its kernels are done from a completion word in the block, not from the stream
+// (`host_tiny_spin`, default 1): a one-key call's one-lane kernel stores a sequence number there last
+// (system-scope release), other calls launch k_done_word behind their kernels, and the host spins on it --
+// 7.2 / 9.6 us against 11.5 us for a one-wave kernel and a stream sync (tools/syncbench.hip).  After 2 ms
+// without it (a queue still busy with earlier work, or a fault) the host waits for the stream, which also
+// reports any error.
 static std::atomic<int> g_tiny_spin{1};
 
-static int tiny_one(rbx_ctx *c, const FilterDesc &f, const KeysDev &dk, bool is_add) {
+static uint32_t tiny_next_seq(rbx_ctx *c) {
     uint32_t seq = ++c->tiny_seq;
     if (seq == 0) seq = c->tiny_seq = 1;
-    auto *h_done = (uint32_t *)(c->pin_tiny + kTinyDoneAt);
-    launch_bloom_one(is_add, dk, fast_len(dk), f, c->pin_tiny_dev, nullptr, (uint32_t *)(c->pin_tiny_dev + kTinyDoneAt),
-                     seq, c->stream);
+    return seq;
+}
+
+// rc: the launches' result; word_launched: seq is on its way (else the call falls back to the stream)
+static int tiny_wait(rbx_ctx *c, int rc, uint32_t seq, bool word_launched) {
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(c->stream);
+    if (rc != RBX_OK || e != hipSuccess || !word_launched) {
+        const hipError_t es = hipStreamSynchronize(c->stream);
+        RBX_TRY(rc);
         HIP_TRY(e);
+        HIP_TRY(es);
+        return RBX_OK;
     }
+    const auto *h_done = (const uint32_t *)(c->pin_tiny + kTinyDoneAt);
     const auto t0 = std::chrono::steady_clock::now();
     while (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-            RBX_TRY(tiny_finish(c, RBX_OK));
+            HIP_TRY(hipStreamSynchronize(c->stream));
             if (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq)
-                return fail(RBX_E_DEVICE, "one-key kernel finished without its completion word");
+                return fail(RBX_E_DEVICE, "tiny call finished without its completion word");
             break;
         }
     }
     return RBX_OK;
+}
+
+// the launches' result -> the completion word behind them (or the stream when spinning is off) -> errors
+static int tiny_done(rbx_ctx *c, int rc) {
+    const bool spin = g_tiny_spin && rc == RBX_OK;
+    const uint32_t seq = spin ? tiny_next_seq(c) : 0;
+    if (spin) launch_done_word((uint32_t *)(c->pin_tiny_dev + kTinyDoneAt), seq, c->stream);
+    return tiny_wait(c, rc, seq, spin);
+}
+
+static int tiny_one(rbx_ctx *c, const FilterDesc &f, const KeysDev &dk, bool is_add) {
+    const uint32_t seq = tiny_next_seq(c);
+    launch_bloom_one(is_add, dk, fast_len(dk), f, c->pin_tiny_dev, nullptr, (uint32_t *)(c->pin_tiny_dev + kTinyDoneAt),
+                     seq, c->stream);
+    return tiny_wait(c, RBX_OK, seq, true);
 }
 
 static int bloom_host_tiny(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rbx_keys *keys, uint8_t *out_flags,
@@ -1377,7 +1390,7 @@ static int bloom_host_tiny(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rb
         if (out_count) *out_count = v;
         return RBX_OK;
     }
-    RBX_TRY(tiny_finish(c, is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_flags, nullptr, nullptr, c->stream)
+    RBX_TRY(tiny_done(c, is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_flags, nullptr, nullptr, c->stream)
                                   : run_contains(c, dk, f, d_flags, nullptr, c->stream)));
     const uint8_t *fl = c->pin_tiny;
     uint64_t cnt = 0;
@@ -2194,7 +2207,7 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
         } else {
             rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
         }
-        RBX_TRY(tiny_finish(c, rc));
+        RBX_TRY(tiny_done(c, rc));
         const uint8_t *fl = c->pin_tiny;
         if (out_counts)
             for (uint32_t q = 0; q < nseg; ++q) {
@@ -2447,7 +2460,7 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         memset(ch_h, 0, (size_t)nseg * 4);
         const KeysDev dk = tiny_stage(c, elements);
         TinyArena ta{c->pin_tiny + kTinyArenaAt, c->pin_tiny_dev + kTinyArenaAt, kTinyArenaBytes, 0};
-        RBX_TRY(tiny_finish(c, pfadd_run(c, hl, seg_offsets, dk, (uint32_t *)(c->pin_tiny_dev + kTinySegAt), c->stream,
+        RBX_TRY(tiny_done(c, pfadd_run(c, hl, seg_offsets, dk, (uint32_t *)(c->pin_tiny_dev + kTinySegAt), c->stream,
                                          &ta)));
         memcpy(ch.data(), ch_h, (size_t)nseg * 4);
         for (uint32_t s = 0; s < nseg; ++s) {

@@ -247,6 +247,8 @@ void launch_bloom_contains(const KeysDev &keys, int klen_fast, const uint32_t *b
 // (run_add, keys.n == 1).  done (nullable): seq is stored there last, at system scope (bloom_host_tiny)
 void launch_bloom_one(bool add, const KeysDev &keys, int klen_fast, const FilterDesc &f, uint8_t *out,
                       unsigned long long *count, uint32_t *done, uint32_t seq, hipStream_t st);
+// one store of seq into done (coherent host memory), after the stream's earlier work
+void launch_done_word(uint32_t *done, uint32_t seq, hipStream_t st);
 // tile_seg0[t] = segment holding key 256*t (precomputed once per multi-tenant batch)
 void launch_tile_seg0(const uint64_t *seg_off, uint32_t nseg, uint64_t nkeys, uint32_t *tile_seg0, hipStream_t st);
 void launch_bloom_contains_multi(const KeysDev &keys, int klen_fast, const FilterDesc *filt,
