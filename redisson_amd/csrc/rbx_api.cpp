@@ -1263,8 +1263,8 @@ static int bloom_host_small(rbx_ctx *c, const FilterDesc &f, uint32_t k, const r
 
 // Tiny host batches -- add(T) / contains(T) and collections of up to host_tiny_keys keys and 64 KiB of key
 // bytes: the keys are copied into coherent (uncached, device-mapped) pinned memory, the kernels read them
-// from there over the host link and write their flags back into it, so the call is its launches and one
-// stream sync: no upload, no readback, no zeroed count word.  Counts are the flags' sums on the host
+// from there over the host link and write their flags back into it, so the call is its launches and a wait
+// for a completion word in the same block: no upload, no readback, no zeroed count word.  Counts are the flags' sums on the host
 // (add(Collection) and contains(Collection) both count the keys whose reply is true,
 // M/RedissonBloomFilter.java:104-137,208-236; per segment for the multi-tenant calls).
 static std::atomic<uint64_t> g_tiny_keys{16384};  // rbx_tune("host_tiny_keys"): 0 = off
@@ -1316,7 +1316,7 @@ static bool bloom_tiny_fits(rbx_ctx *c, const rbx_keys *keys) {
     return true;
 }
 
-// the keys into the block (the previous call synced before returning); their device view
+// the keys into the block (the previous call's kernels were done when it returned: tiny_wait); their device view
 static KeysDev tiny_stage(rbx_ctx *c, const rbx_keys *keys) {
     uint8_t *hp = c->pin_tiny, *dp = c->pin_tiny_dev;
     const uint64_t n = keys->n, b0 = keys->offsets ? keys->offsets[0] : 0;
@@ -1364,9 +1364,10 @@ static int tiny_wait(rbx_ctx *c, int rc, uint32_t seq, bool word_launched) {
     return RBX_OK;
 }
 
-// the launches' result -> the completion word behind them (or the stream when spinning is off) -> errors
-static int tiny_done(rbx_ctx *c, int rc) {
-    const bool spin = g_tiny_spin && rc == RBX_OK;
+// the launches' result -> the completion word behind them (or the stream when spinning is off) -> errors;
+// spin: host_tiny_spin as the call read it
+static int tiny_done(rbx_ctx *c, int rc, bool spin) {
+    spin = spin && rc == RBX_OK;
     const uint32_t seq = spin ? tiny_next_seq(c) : 0;
     if (spin) launch_done_word((uint32_t *)(c->pin_tiny_dev + kTinyDoneAt), seq, c->stream);
     return tiny_wait(c, rc, seq, spin);
@@ -1383,7 +1384,8 @@ static int bloom_host_tiny(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rb
                            uint64_t *out_count, bool is_add) {
     const KeysDev dk = tiny_stage(c, keys);
     uint8_t *d_flags = c->pin_tiny_dev;
-    if (keys->n == 1 && f.k <= 16 && g_tiny_spin && (!is_add || g_add_one)) {
+    const bool spin = g_tiny_spin;  // once per call
+    if (keys->n == 1 && f.k <= 16 && spin && (!is_add || g_add_one)) {
         RBX_TRY(tiny_one(c, f, dk, is_add));
         const uint8_t v = c->pin_tiny[0];
         if (out_flags) out_flags[0] = v;
@@ -1391,7 +1393,7 @@ static int bloom_host_tiny(rbx_ctx *c, const FilterDesc &f, uint32_t k, const rb
         return RBX_OK;
     }
     RBX_TRY(tiny_done(c, is_add ? run_add(c, dk, nullptr, nullptr, 0, f, k, d_flags, nullptr, nullptr, c->stream)
-                                  : run_contains(c, dk, f, d_flags, nullptr, c->stream)));
+                                  : run_contains(c, dk, f, d_flags, nullptr, c->stream), spin));
     const uint8_t *fl = c->pin_tiny;
     uint64_t cnt = 0;
     for (uint64_t i = 0; i < keys->n; ++i) cnt += fl[i];
@@ -2207,7 +2209,7 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
         } else {
             rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
         }
-        RBX_TRY(tiny_done(c, rc));
+        RBX_TRY(tiny_done(c, rc, g_tiny_spin));
         const uint8_t *fl = c->pin_tiny;
         if (out_counts)
             for (uint32_t q = 0; q < nseg; ++q) {
@@ -2461,7 +2463,8 @@ static int hll_add_multi(rbx_ctx *c, const std::vector<std::string> &names, cons
         const KeysDev dk = tiny_stage(c, elements);
         TinyArena ta{c->pin_tiny + kTinyArenaAt, c->pin_tiny_dev + kTinyArenaAt, kTinyArenaBytes, 0};
         RBX_TRY(tiny_done(c, pfadd_run(c, hl, seg_offsets, dk, (uint32_t *)(c->pin_tiny_dev + kTinySegAt), c->stream,
-                                         &ta)));
+                                       &ta),
+                          g_tiny_spin));
         memcpy(ch.data(), ch_h, (size_t)nseg * 4);
         for (uint32_t s = 0; s < nseg; ++s) {
             if (ch[s]) hl[s]->card |= 1ULL << 63;  // HLL_INVALIDATE_CACHE
