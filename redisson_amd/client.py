@@ -32,6 +32,21 @@ def _is_collection(x) -> bool:
     return isinstance(x, (list, tuple)) or (isinstance(x, Collection) and not isinstance(x, (str, bytes, bytearray)))
 
 
+
+class _OneKey:
+    """add(T) / contains(T): one encoded key as an rbx_keys of stride len(key) over the bytes object itself
+    (no numpy arena; the bytes object stays referenced for the call)."""
+
+    __slots__ = ("key", "n", "struct")
+
+    def __init__(self, key: bytes):
+        self.key = key if type(key) is bytes else bytes(key)
+        self.n = 1
+        self.struct = L.RbxKeys(C.cast(C.c_char_p(self.key), C.c_void_p).value, None, len(self.key), 1)
+
+    def ptr(self):
+        return C.byref(self.struct)
+
 class RedissonClient:
     """Redisson.create(...) for one GPU (M/Redisson.java).  One engine context per device."""
 
@@ -203,10 +218,13 @@ class RBloomFilter(_Expirable):
     def _encode_all(self, objects) -> Arena:
         return Arena([self._codec.encode(o) for o in objects])
 
+    def _one(self, obj) -> "_OneKey":
+        return _OneKey(self._codec.encode(obj))
+
     def _batch(self, fn, objects, flags: bool):
         if self._size == 0:  # :106-108
             self._read_config()
-        a = objects if isinstance(objects, Arena) else self._encode_all(objects)
+        a = objects if isinstance(objects, (Arena, _OneKey)) else self._encode_all(objects)
         out = np.zeros(max(a.n, 1), np.uint8) if flags else None
         cnt = C.c_uint64()
         _check(fn(self._client.ctx, self._bname(), self._size, self._k, a.ptr(),
@@ -217,13 +235,13 @@ class RBloomFilter(_Expirable):
         """add(T) -> bool  |  add(Collection<T>) -> long  (:99-137)"""
         if isinstance(objects, Arena) or _is_collection(objects):
             return self._batch(L.lib().rbx_bloom_add, objects, False)
-        return self._batch(L.lib().rbx_bloom_add, [objects], False) > 0
+        return self._batch(L.lib().rbx_bloom_add, self._one(objects), False) > 0
 
     def contains(self, objects):
         """contains(T) -> bool  |  contains(Collection<T>) -> long  (:153-201)"""
         if isinstance(objects, Arena) or _is_collection(objects):
             return self._batch(L.lib().rbx_bloom_contains, objects, False)
-        return self._batch(L.lib().rbx_bloom_contains, [objects], False) > 0
+        return self._batch(L.lib().rbx_bloom_contains, self._one(objects), False) > 0
 
     def addEach(self, objects):
         """(count, per-key 'newly added' flags) -- engine extension of add(Collection)."""
@@ -421,11 +439,11 @@ class RHyperLogLog(_Expirable):
 
     def add(self, obj) -> bool:
         """:71-73 PFADD name e"""
-        return self.addAll([obj])
+        return self.addAll(_OneKey(self._codec.encode(obj)))
 
     def addAll(self, objects) -> bool:
         """:76-81 PFADD name e1..en"""
-        a = objects if isinstance(objects, Arena) else Arena([self._codec.encode(o) for o in objects])
+        a = objects if isinstance(objects, (Arena, _OneKey)) else Arena([self._codec.encode(o) for o in objects])
         ch = C.c_int()
         _check(L.lib().rbx_hll_add(self._client.ctx, self._name.encode(), a.ptr(), C.byref(ch)))
         return bool(ch.value)

@@ -317,8 +317,10 @@ def main():
             if nb <= 4096:
                 calls["add_host_new"] = add_host_new(0)
                 calls["add_dev_new"] = add_dev_new(0)
-            if nb == 1:
+            if nb == 1:  # the Python object forms (one encoded key, no arena)
+                one_new = [bytes(r) for r in rng.integers(0, 256, size=(320, 16), dtype=np.uint8)]
                 calls["contains_one_object"] = lambda i: fb.contains(bytes(hostkeys[0]))
+                calls["add_one_object_new"] = lambda i: fb.add(one_new[i])
             if nb >= 4 and nb <= 4096:  # one multi-tenant host call over 4 filters (an RBatch of 4 collections)
                 from redisson_amd import bloom_add_multi, bloom_contains_multi
 
@@ -337,6 +339,8 @@ def main():
                 calls["pfadd_sparse_host"] = lambda i: client.getHyperLogLog(f"sb-hs-{nb}-{i // 20}").addAll(
                     adds[i % 20])
                 calls["pfcount_dense_host"] = lambda i: hd.count()
+                if nb == 1:
+                    calls["pfadd_one_object"] = lambda i: hd.add(one_new[i])
             # the tiny path (bloom_host_tiny, <= host_tiny_keys keys) and the one-segment add
             # (add_single_seg_keys) against the r05 paths
             def off(fn, *knobs):
