@@ -20,7 +20,7 @@ import numpy as np
 from . import _lib as L
 from .codec import DEFAULT_CODEC, Codec
 from .exceptions import IllegalArgumentException, raise_for
-from .keys import Arena
+from .keys import Arena, _OneKey
 
 
 def _check(rc: int) -> None:
@@ -31,21 +31,6 @@ def _check(rc: int) -> None:
 def _is_collection(x) -> bool:
     return isinstance(x, (list, tuple)) or (isinstance(x, Collection) and not isinstance(x, (str, bytes, bytearray)))
 
-
-
-class _OneKey:
-    """add(T) / contains(T): one encoded key as an rbx_keys of stride len(key) over the bytes object itself
-    (no numpy arena; the bytes object stays referenced for the call)."""
-
-    __slots__ = ("key", "n", "struct")
-
-    def __init__(self, key: bytes):
-        self.key = key if type(key) is bytes else bytes(key)
-        self.n = 1
-        self.struct = L.RbxKeys(C.cast(C.c_char_p(self.key), C.c_void_p).value, None, len(self.key), 1)
-
-    def ptr(self):
-        return C.byref(self.struct)
 
 class RedissonClient:
     """Redisson.create(...) for one GPU (M/Redisson.java).  One engine context per device."""

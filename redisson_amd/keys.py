@@ -36,6 +36,21 @@ class Arena:
         return C.byref(self.struct)
 
 
+class _OneKey:
+    """add(T) / contains(T): one encoded key as an rbx_keys of stride len(key) over the bytes object itself
+    (no numpy arena; the bytes object stays referenced for the call)."""
+
+    __slots__ = ("key", "n", "struct")
+
+    def __init__(self, key: bytes):
+        self.key = key if type(key) is bytes else bytes(key)
+        self.n = 1
+        self.struct = L.RbxKeys(C.cast(C.c_char_p(self.key), C.c_void_p).value, None, len(self.key), 1)
+
+    def ptr(self):
+        return C.byref(self.struct)
+
+
 def device_keys(data_ptr: int, n: int, stride: int = 0, offsets_ptr: int | None = None) -> L.RbxKeys:
     """rbx_keys over DEVICE memory (e.g. torch tensor data_ptr())."""
     return L.RbxKeys(data_ptr, offsets_ptr, stride, n)

@@ -17,7 +17,7 @@ import numpy as np
 from . import _lib as L
 from .client import _check, _is_collection
 from .codec import DEFAULT_CODEC, Codec
-from .keys import Arena
+from .keys import Arena, _OneKey
 
 
 class RedissonNode:
@@ -121,7 +121,7 @@ class NodeBloomFilter:
     def _batch(self, fn, objects, flags):
         if self._size == 0:
             self._read_config()
-        a = objects if isinstance(objects, Arena) else Arena([self._codec.encode(o) for o in objects])
+        a = objects if isinstance(objects, (Arena, _OneKey)) else Arena([self._codec.encode(o) for o in objects])
         s, keep = self._n()
         out = np.zeros(max(a.n, 1), np.uint8) if flags else None
         cnt = C.c_uint64()
@@ -147,12 +147,12 @@ class NodeBloomFilter:
     def add(self, objects):
         if isinstance(objects, Arena) or _is_collection(objects):
             return self._batch(L.lib().rbx_node_bloom_add, objects, False)
-        return self._batch(L.lib().rbx_node_bloom_add, [objects], False) > 0
+        return self._batch(L.lib().rbx_node_bloom_add, _OneKey(self._codec.encode(objects)), False) > 0
 
     def contains(self, objects):
         if isinstance(objects, Arena) or _is_collection(objects):
             return self._batch(L.lib().rbx_node_bloom_contains, objects, False)
-        return self._batch(L.lib().rbx_node_bloom_contains, [objects], False) > 0
+        return self._batch(L.lib().rbx_node_bloom_contains, _OneKey(self._codec.encode(objects)), False) > 0
 
     def containsEach(self, objects):
         return self._batch(L.lib().rbx_node_bloom_contains, objects, True)
