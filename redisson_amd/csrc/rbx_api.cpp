@@ -1872,6 +1872,28 @@ static int upload_filters(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, 
     return RBX_OK;
 }
 
+// d_tile_seg0 (nullable): each 256-key tile's first segment, already in device-visible memory (the tiny host
+// path computes it on the host); else k_tile_seg0 finds it
+static int contains_multi_run(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, const uint64_t *d_seg_offsets,
+                              const rbx_keys *d_keys, uint8_t *d_out, unsigned long long *d_counts, hipStream_t st,
+                              const uint32_t *d_tile_seg0) {
+    uint32_t kmax;
+    uint64_t bytes = 0;
+    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, false, &bytes));
+    if (d_keys->n == 0) return RBX_OK;
+    KeysDev k = keys_dev(d_keys);
+    if (!d_tile_seg0) {
+        RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
+        launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+        d_tile_seg0 = c->tile_segs.as<uint32_t>();
+    }
+    const bool slots = g_multi_slots == 1 || (g_multi_slots == 2 && bytes >= kSlotsMinBytes);
+    launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg, d_tile_seg0, kmax,
+                                d_out, d_counts, st, slots);
+    HIP_TRY(hipGetLastError());
+    return RBX_OK;
+}
+
 int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg,
                                  const uint64_t *d_seg_offsets, const rbx_keys *d_keys, uint8_t *d_out,
                                  unsigned long long *d_counts, void *stream) {
@@ -1880,19 +1902,7 @@ int rbx_bloom_contains_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t
     std::lock_guard<std::recursive_mutex> g(c->ks.mu);
     RBX_TRY(set_device(c));
     ScratchOrder so_(c, pick_stream(c, stream));
-    hipStream_t st = pick_stream(c, stream);
-    uint32_t kmax;
-    uint64_t bytes = 0;
-    RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, false, &bytes));
-    if (d_keys->n == 0) return RBX_OK;
-    KeysDev k = keys_dev(d_keys);
-    RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
-    launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
-    const bool slots = g_multi_slots == 1 || (g_multi_slots == 2 && bytes >= kSlotsMinBytes);
-    launch_bloom_contains_multi(k, fast_len(k), c->filt_table.as<FilterDesc>(), d_seg_offsets, nseg,
-                                c->tile_segs.as<uint32_t>(), kmax, d_out, d_counts, st, slots);
-    HIP_TRY(hipGetLastError());
-    return RBX_OK;
+    return contains_multi_run(c, filters, nseg, d_seg_offsets, d_keys, d_out, d_counts, pick_stream(c, stream), nullptr);
 }
 
 // rbx_tune("stream_chunk", n) caps a chunk of the ordered stream and of the 8-byte multi-tenant add at
@@ -1989,8 +1999,12 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
     RBX_TRY(upload_filters(c, filters, nseg, &kmax, st, true));
     if (d_keys->n == 0) return RBX_OK;
     KeysDev k = keys_dev(d_keys);
-    RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
-    launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+    // the chunked and table paths find each tile's first segment in tile_seg0 (the per-segment kernel does not)
+    auto tiles = [&]() -> int {
+        RBX_TRY(c->tile_segs.reserve(((d_keys->n + 255) / 256) * 4));
+        launch_tile_seg0(d_seg_offsets, nseg, d_keys->n, c->tile_segs.as<uint32_t>(), st);
+        return RBX_OK;
+    };
     uint32_t bb = 1, fbits = 0;
     while ((1ULL << bb) < c->filt_maxbits) ++bb;
     while ((1ULL << fbits) < c->filt_nfids) ++fbits;
@@ -2002,7 +2016,10 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
         // then handles only segments past segmax
         RBX_TRY(c->madd_c.reserve((8ULL << lgc) + 64));
         uint32_t *big = (uint32_t *)(c->madd_c.as<unsigned long long>() + (1ULL << lgc)) + 4;
-        HIP_TRY(hipMemsetAsync(big, 0, 4, st));
+        // no segment past segmax (known from the host, or the batch is that short): the flag is never
+        // raised nor read, so it needs no zeroing launch
+        const bool may_big = !(c->madd_maxseg_hint <= segmax || d_keys->n <= segmax);
+        if (may_big) HIP_TRY(hipMemsetAsync(big, 0, 4, st));
         MaddSegArgs a{};
         a.keys = k;
         a.filt = c->filt_table.as<FilterDesc>();
@@ -2016,7 +2033,7 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
         a.big = big;
         launch_madd_seg(a, fast_len(k), st);
         HIP_TRY(hipGetLastError());
-        if (c->madd_maxseg_hint <= segmax || d_keys->n <= segmax) return RBX_OK;  // no long segment
+        if (!may_big) return RBX_OK;  // no long segment
         // device offsets: read the flag (one sync) rather than launch the chunked path's kernels for
         // nothing -- 60 empty launches per C3 call in r05
         HIP_TRY(hipMemcpyAsync(c->pin_word, big, 4, hipMemcpyDeviceToHost, st));  // pinned: no staging copy
@@ -2024,9 +2041,11 @@ int rbx_bloom_add_multi_dev(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg
         uint32_t has_big;
         memcpy(&has_big, c->pin_word, 4);
         if (!has_big) return RBX_OK;
+        RBX_TRY(tiles());
         return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, lgc, big,
                               segmax);
     }
+    RBX_TRY(tiles());
     if (mode && kmax <= 32 && bb + fbits <= 41)
         return run_add_multi8(c, k, d_seg_offsets, nseg, kmax, bb, 64 - bb - fbits, d_out_new, d_counts, st, lgc);
     FilterDesc dummy{};
@@ -2207,7 +2226,15 @@ static int multi_host(rbx_ctx *c, rbx_bloom *const *filters, uint32_t nseg, cons
             rc = rbx_bloom_add_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
             c->madd_maxseg_hint = ~0ULL;
         } else {
-            rc = rbx_bloom_contains_multi_dev(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream);
+            // each 256-key tile's first segment from the host (no k_tile_seg0 launch)
+            std::vector<uint32_t> ts((keys->n + 255) / 256);
+            for (uint32_t q = 0, t = 0; t < ts.size(); ++t) {
+                while (seg_offsets[q + 1] <= (uint64_t)t * 256) ++q;
+                ts[t] = q;
+            }
+            TinyArena ta{c->pin_tiny + kTinyArenaAt, c->pin_tiny_dev + kTinyArenaAt, kTinyArenaBytes, 0};
+            rc = contains_multi_run(c, filters, nseg, d_seg, &kd, d_flags, nullptr, c->stream,
+                                    (const uint32_t *)ta.put(ts.data(), ts.size() * 4));
         }
         RBX_TRY(tiny_done(c, rc, g_tiny_spin));
         const uint8_t *fl = c->pin_tiny;
