@@ -1030,8 +1030,8 @@ def test_host_tiny_batches(client, fresh, tiny, seg, one, spin, k_fpp):
     """r06: host batches of <= host_tiny_keys keys and <= 64 KiB of key bytes run from coherent pinned memory
     (bloom_host_tiny: the kernel reads the keys over the host link and writes the flags back), and
     single-filter adds of <= add_single_seg_keys keys run the per-segment kernel on one segment, and one-key
-    adds k_bloom_add_one (add_one_key), and one-key host calls spin on the kernel's completion word
-    (host_tiny_spin); each on and off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
+    adds k_bloom_add_one (add_one_key), and small host calls spin on a completion word (host_tiny_spin);
+    each on and off: single keys, a key repeated inside one batch (only its first occurrence is new), 255 / 256 / 4,096
     (= 64 KiB) / 4,097 keys, 16,384 short keys, variable-length and empty keys -- per-key flags and counts,
     then the bitmap and the Redis string length, vs the oracle."""
     from redisson_amd import _lib as L_
@@ -1043,7 +1043,7 @@ def test_host_tiny_batches(client, fresh, tiny, seg, one, spin, k_fpp):
     dup = rng.integers(0, 256, size=(64, 16), dtype=np.uint8)
     dup[40] = dup[3]
     dup[63] = dup[3]
-    mats = [rng.integers(0, 256, size=(n, 16), dtype=np.uint8) for n in (1, 255, 256, 4096, 4097)] + [dup] + \
+    mats = [rng.integers(0, 256, size=(n, 16), dtype=np.uint8) for n in (1, 2, 17, 63, 64, 65, 255, 256, 4096, 4097)] + [dup] + \
            [rng.integers(0, 256, size=(16384, 4), dtype=np.uint8)]
     var = [[rng.bytes(int(x)) for x in rng.integers(0, 91, size=300)], [b""] * 5,
            [b"k-%d" % (i % 7) for i in range(50)]]  # repeats inside the batch
@@ -1062,7 +1062,7 @@ def test_host_tiny_batches(client, fresh, tiny, seg, one, spin, k_fpp):
             assert cg == cr and np.array_equal(ng, nr)
             assert f.add(a) == ref.add(*o)  # again: nothing new, count only
             assert f.contains(a) == ref.contains(*o)
-        for key in [bytes(mats[3][9]), b"never-added-key", b""] + [rng.bytes(int(x)) for x in rng.integers(0, 80, 40)]:
+        for key in [bytes(mats[8][9]), b"never-added-key", b""] + [rng.bytes(int(x)) for x in rng.integers(0, 80, 40)]:
             assert f.contains(Arena([key])) == ref.contains(*O.arena([key]))
             assert f.add(Arena([key])) == ref.add(*O.arena([key]))
     finally:

@@ -293,7 +293,7 @@ def main():
         tiny_keys, seg_keys = a.tiny_keys, a.seg_keys
         assert L.lib().rbx_tune(b"host_tiny_keys", tiny_keys) == 0
         assert L.lib().rbx_tune(b"add_single_seg_keys", seg_keys) == 0
-        for nb in [1, 16, 256, 1024, 4096, 65536]:
+        for nb in [1, 16, 64, 256, 1024, 4096, 65536]:
             res = {}
             present = Arena.fixed(hostkeys[:nb])
             adds = [Arena.fixed(rng.integers(0, 256, size=(nb, 16), dtype=np.uint8)) for _ in range(20)]
